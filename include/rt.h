@@ -1,0 +1,177 @@
+/*
+ * rt.h — C ABI of the MI355X-native per-pixel render loop.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (keychera/raytracing-clj, Clojure, no FFI of its own). It replaces:
+ *
+ *   compute-pixel + the row-chunk executor   src/raytracing.clj:141-171
+ *     └ ray-color (recursive bounce)         src/raytracing.clj:45-58
+ *        └ hit-anything (closest-hit scan)   src/raytracing.clj:33-43
+ *           └ sphere ::hit-fn                src/hittable.clj:7-31
+ *        └ material ::scatter-fn             src/material.clj:13-46
+ *           (lambertian :13-19, metal :21-28, dielectric :34-46)
+ *        └ vec3a math + rand samplers        src/vec3a.clj:56-101
+ *
+ * Scene definition (raytracing.clj:63-78), camera set-up (:101-139) and the
+ * PPM writer (:19-26, :172-175) stay on the host; helpers for them are
+ * exported here too (rt_camera_setup, rt_quantize, rt_write_ppm) so a
+ * Clojure/JNI, C++ or Python host can reuse them.
+ *
+ * Conventions: plain pointers and sizes, no ownership transfer (the library
+ * never retains a caller pointer past the call), 0 = OK, negative = error
+ * (see rt_status; message via rt_last_error(), thread-local).
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+typedef enum rt_status {
+  RT_OK = 0,
+  RT_E_ARG = -1,        /* bad argument (NULL, size, range)                      */
+  RT_E_MATERIAL = -2,   /* unsupported material kind                             */
+  RT_E_TOO_MANY = -3,   /* sphere list larger than the LDS-resident limit        */
+  RT_E_HIP = -4,        /* HIP runtime error (message has the HIP error string)  */
+  RT_E_NODEV = -5,      /* no GPU visible / device index out of range            */
+  RT_E_IO = -6          /* file I/O (rt_write_ppm)                               */
+} rt_status;
+
+/* ---- material kinds: material.clj:13 (lambertian), :21 (metal), :34 (dielectric).
+ * RT_NONE: a body merged with no material: ray-color finds no scatter-fn and
+ * returns black (raytracing.clj:49-54). */
+enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_NONE = 3 };
+
+/* Maximum spheres per scene (LDS-resident sphere table, 16 B each). */
+#define RT_MAX_SPHERES 8192
+
+/* ---- scene: the reference's `hittables` vector (raytracing.clj:63-78) -----
+ * Bodies are tested in array order; on equal t the earlier body wins, exactly
+ * as hit-anything's strict `root < closest-so-far` (raytracing.clj:35-42,
+ * hittable.clj:17-23). */
+typedef struct rt_scene {
+  int n;                  /* number of bodies                                  */
+  const float* sphere;    /* n x 4: center x,y,z, radius  (hittable.clj:7)     */
+  const int* mat_kind;    /* n: RT_LAMBERTIAN | RT_METAL | RT_DIELECTRIC | RT_NONE */
+  const float* mat;       /* n x 4: albedo r,g,b, then fuzz (metal) or
+                             refraction index (dielectric); unused lanes 0     */
+} rt_scene;
+
+/* ---- camera: the values -main derives at raytracing.clj:117-139 ---------- */
+typedef struct rt_camera {
+  float center[3];        /* camera-center = look-from          (:126)          */
+  float p00[3];           /* pixel-00-loc                       (:135)          */
+  float du[3];            /* pixel-du                           (:129)          */
+  float dv[3];            /* pixel-dv                           (:130)          */
+  float disk_u[3];        /* defocus-disk-u                     (:138)          */
+  float disk_v[3];        /* defocus-disk-v                     (:139)          */
+  int defocus;            /* defocus-angle > 0                  (:147)          */
+} rt_camera;
+
+/* ---- render parameters -----------------------------------------------------
+ * Pixel (i, j) of sample k gets its own RNG stream keyed by (seed, j*width+i,
+ * sample_begin+k): results do not depend on tiling, device count or launch
+ * shape.  spp / max_depth are the reference's CLI args (raytracing.clj:96-97).
+ *
+ * Output rows: the rendered rows are [row_begin, row_end).  With
+ * tile_step == 0 they are written contiguously.  With tile_step > 0 the call
+ * renders only the interleaved row tiles  tile_first, tile_first+tile_step,
+ * ... (tile height row_tile, tiles counted from row_begin) and writes them
+ * compacted, in order; rt_rows_out() gives the row count. */
+typedef struct rt_params {
+  int width, height;      /* full image; height = int(width/aspect) (:105-107) */
+  int row_begin, row_end; /* global rows to render                             */
+  int spp;                /* samples per pixel in this call                    */
+  int max_depth;          /* ray-color depth budget                            */
+  uint64_t seed;          /* RNG key                                           */
+  int sample_begin;       /* first sample index (sample stripes), usually 0    */
+  int n_devices;          /* rt_render fan-out: 0 = all visible devices        */
+  int row_tile;           /* interleaved tile height (rows); 0 -> 8            */
+  int tile_first;         /* rt_launch: first tile of this shard               */
+  int tile_step;          /* rt_launch: tile stride (0 = contiguous rows)      */
+  int flags;              /* reserved, must be 0                               */
+} rt_params;
+
+/* ---- per-call statistics (device-side counters) ------------------------- */
+typedef struct rt_stats {
+  uint64_t segments;      /* hit-anything calls (raytracing.clj:48)            */
+  uint64_t samples;       /* compute-pixel loop iterations (:142-154)          */
+  double kernel_ms;       /* max over devices of the trace-kernel time         */
+  double total_ms;        /* wall time of the whole call incl. H2D/D2H         */
+  int n_devices;          /* devices used                                      */
+} rt_stats;
+
+/* ========================= host-side helpers =========================== */
+
+/* Camera basis exactly as -main computes it, in double, rounded to float at
+ * the end (raytracing.clj:105-139; deg->rad :60-61).  vfov/defocus_angle in
+ * degrees.  Viewport width uses image_width/image_height, not the aspect
+ * ratio (:120). */
+int rt_camera_setup(int image_width, int image_height, double vfov,
+                    const double look_from[3], const double look_at[3],
+                    const double vup[3], double defocus_angle,
+                    double focus_dist, rt_camera* out);
+
+/* write-color! per channel (raytracing.clj:19-26):
+ * out = int(256 * clamp(c > 0 ? sqrt(c) : 0, 0, 0.999)); NaN -> 0.  n = channel count. */
+int rt_quantize(const float* lin, uint8_t* out, size_t n);
+
+/* PPM P3, one "r g b\n" per pixel, rows top->bottom (raytracing.clj:172-175). */
+int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
+
+/* Number of output rows a (row_begin,row_end,row_tile,tile_first,tile_step)
+ * selection produces (0 on bad args). */
+int rt_rows_out(const rt_params* p);
+
+/* ---- scene builders (host) ----------------------------------------------
+ * Both write up to `cap` bodies into sphere (x4), kind, mat (x4) and return
+ * the body count (the needed count when the arrays are NULL / cap too small).
+ *
+ * rt_scene_reference: the reference's five bodies, in order
+ *   (raytracing.clj:63-78): ground, center, left (glass), bubble, right (metal).
+ * rt_scene_cover: the RTIOW "final render" cover scene (book §14; the
+ *   reference has no such scene): ground r=1000, a
+ *   (2*grid)^2 jittered field of r=0.2 bodies (80 % lambertian, 15 % metal,
+ *   5 % glass; skipped within 0.9 of (4,0.2,0)), then three r=1 bodies.
+ *   Deterministic in `seed` (splitmix64 stream, 53-bit doubles). */
+int rt_scene_reference(float* sphere, int* kind, float* mat, int cap);
+int rt_scene_cover(int grid, uint64_t seed, float* sphere, int* kind, float* mat, int cap);
+
+/* ============================ rendering ================================ */
+
+/* Render into a caller-owned host buffer of linear RGB fp32, row-major,
+ * rows_out x width x 3, the mean over spp (compute-pixel's accum/spp,
+ * raytracing.clj:155).  Fans out over p->n_devices GPUs inside the call
+ * (one host thread per device, interleaved row tiles, host-side gather; no
+ * collectives).  tile_first/tile_step must be 0 here.  stats may be NULL. */
+int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p,
+              float* out_rgb, size_t out_len, rt_stats* stats);
+
+/* Device-resident path (inputs already in HBM; used by the benchmark). */
+typedef struct rt_dscene rt_dscene;
+int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out);
+int rt_scene_free(rt_dscene* ds);
+/* Asynchronous: enqueue one trace launch on hip_stream (NULL = default
+ * stream) of ds's device.  d_out: device buffer of rt_rows_out(p) x width x 3
+ * floats.  d_counters: NULL or device u64[2] += {segments, samples}. */
+int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
+              float* d_out, uint64_t* d_counters, void* hip_stream);
+
+/* Kernel variant selector for A/B measurement: 0 = default, 1 = sphere table
+ * in LDS, 2 = sphere table through the scalar (constant) cache.  Returns the
+ * previous value; applies to subsequent launches in this process. */
+int rt_set_variant(int variant);
+
+int rt_device_count(void);
+const char* rt_last_error(void);
+const char* rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_H */

@@ -1,0 +1,7 @@
+"""TEST INFRASTRUCTURE ONLY — the parity oracle (see rt_oracle.cpp header).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this.  The product (raytracing-clj_amd/) never does.
+"""
+from .oracle import MODE_MIRROR32, MODE_REF64, build, render, sphere_hit, reflect, refract, reflectance, \
+    quantize, camera, rng_stream  # noqa: F401

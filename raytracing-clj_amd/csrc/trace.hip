@@ -1,0 +1,482 @@
+// trace.hip — the per-pixel render loop as one stackless gfx950 kernel.
+//
+// Replaces, for one launch, the reference's
+//   compute-pixel spp loop            src/raytracing.clj:141-155
+//   ray-color (recursive)             src/raytracing.clj:45-58
+//   hit-anything (closest-hit scan)   src/raytracing.clj:33-43
+//   sphere ::hit-fn                   src/hittable.clj:7-31
+//   lambertian / metal / dielectric   src/material.clj:13-46
+//   vec3a math, rand samplers         src/vec3a.clj:56-101
+//
+// Execution shape (MI355X / CDNA4):
+//   * one lane = one pixel; one wave = an 8x8 pixel tile (ray coherence for
+//     camera rays); one 256-thread workgroup = 16x16 pixels;
+//   * the lane runs its spp samples back to back with *sample regeneration*:
+//     when a path ends (sky / absorbed / depth) the lane accumulates and
+//     starts its next camera sample in the same loop iteration structure, so
+//     a wave keeps all 64 lanes busy until its pixels run out of samples;
+//   * ray-color's recursion becomes a throughput accumulator T (stackless);
+//   * the sphere table (centre, -r^2: 16 B per body) is staged once per
+//     workgroup in LDS (variant 1) or read through the scalar cache into
+//     SGPRs (variant 2); the hit test loop is wave-uniform (every lane scans
+//     every body in order), only the rare "line meets sphere" block diverges;
+//   * per-lane xorshift32 RNG, seeded per (seed, pixel, sample) by a hash;
+//   * the framebuffer is written once per pixel (fp32 RGB, 12 B).
+//
+// Arithmetic contract (fp32; mirrored op-for-op by the oracle's fp32 mode,
+// oracle/rt_oracle.cpp, so GPU and CPU agree bit-for-bit): every fused
+// multiply-add is an explicit fmaf, the file is compiled with
+// -ffp-contract=off, division and sqrt are IEEE correctly rounded (HIP's
+// default), and no transcendental function is used.  See DESIGN.md §3.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rtclj {
+
+struct alignas(16) KArgs {
+  const float4* geo;   // n: cx, cy, cz, -r*r   (hit test)
+  const float4* sph;   // n: cx, cy, cz, r      (hit record)
+  const float4* mat;   // n: albedo rgb, fuzz | refraction index
+  const int* kind;     // n: material kind
+  float* out;          // rows_out x width x 3
+  unsigned long long* counters;  // NULL or [segments, samples]
+  float cam[18];       // center, p00, du, dv, disk_u, disk_v
+  int defocus;
+  int n;
+  int width;
+  int rows_out;
+  int row_begin, row_tile, tile_first, tile_step;
+  int spp, sample_begin, max_depth;
+  uint32_t key;
+};
+
+// ---------------------------------------------------------------- RNG ----
+// xorshift32 (Marsaglia 13/17/5); a uniform double of the reference
+// (clojure.core/rand, vec3a.clj:71-72) becomes the top 24 bits / 2^24,
+// i.e. a float in [0, 1) on a 2^-24 grid.
+__device__ __forceinline__ float rng_uniform(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return static_cast<float>(s >> 8) * 0x1p-24f;
+}
+
+// rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32.
+__device__ __forceinline__ float rng_sym(uint32_t& s) {
+  return 2.0f * rng_uniform(s) - 1.0f;
+}
+
+// vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
+// 0 < |v|^2 <= 1 (1e-160 underflows to 0 in fp32), then v / |v|.
+__device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z) {
+  float l2;
+  do {
+    x = rng_sym(s);
+    y = rng_sym(s);
+    z = rng_sym(s);
+    l2 = fmaf(z, z, fmaf(y, y, x * x));
+  } while (!(l2 > 0.0f && l2 <= 1.0f));
+  const float len = sqrtf(l2);
+  x = x / len;
+  y = y / len;
+  z = z / len;
+}
+
+// ------------------------------------------------------------- kernel ----
+enum { SRC_LDS = 1, SRC_SCALAR = 2 };
+
+template <int SRC>
+__global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
+  const int n = a.n;
+  if constexpr (SRC == SRC_LDS) {
+    for (int i = threadIdx.x; i < n; i += 256) s_geo[i] = a.geo[i];
+    __syncthreads();
+  }
+
+  // lane -> pixel: wave w of the block owns the 8x8 tile (w&1, w>>1).
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+  const int ro = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  bool active = (px < a.width) && (ro < a.rows_out);
+
+  // compacted output row -> global image row (interleaved row tiles)
+  int gy = a.row_begin + ro;
+  if (a.tile_step > 0) {
+    const int t = ro / a.row_tile;
+    gy = a.row_begin + (a.tile_first + t * a.tile_step) * a.row_tile + (ro - t * a.row_tile);
+  }
+
+  const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
+  const uint32_t pkey = mix32(a.key ^ mix32(static_cast<uint32_t>(gy) * static_cast<uint32_t>(a.width) +
+                                            static_cast<uint32_t>(px)));
+
+  float accr = 0.0f, accg = 0.0f, accb = 0.0f;
+  uint32_t segs = 0;
+  int k = 0;
+  if (a.spp <= 0 || a.max_depth <= 0) active = false;  // ray-color depth<=0 -> black (:46-47)
+
+  // path state
+  uint32_t st = 0;
+  float ox = 0, oy = 0, oz = 0, dx = 0, dy = 0, dz = 0;
+  float tr = 1, tg = 1, tb = 1;
+  int rem = 0;
+  int last = -1;   // body the current ray leaves (-1: camera ray)
+  bool fresh = true;
+
+  while (active) {
+    if (fresh) {
+      // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
+      st = mix32(pkey + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
+      if (st == 0) st = 0x6d2b79f5u;
+      const float fx = static_cast<float>(px) + (rng_uniform(st) - 0.5f);
+      const float fy = static_cast<float>(gy) + (rng_uniform(st) - 0.5f);
+      const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
+      const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
+      const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
+      if (a.defocus) {
+        // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
+        float qx, qy;
+        do {
+          qx = rng_sym(st);
+          qy = rng_sym(st);
+        } while (!(fmaf(qy, qy, qx * qx) < 1.0f));
+        ox = fmaf(a.cam[15], qy, fmaf(a.cam[12], qx, cx));
+        oy = fmaf(a.cam[16], qy, fmaf(a.cam[13], qx, cy));
+        oz = fmaf(a.cam[17], qy, fmaf(a.cam[14], qx, cz));
+      } else {
+        ox = cx;
+        oy = cy;
+        oz = cz;
+      }
+      dx = sx - ox;
+      dy = sy - oy;
+      dz = sz - oz;
+      tr = tg = tb = 1.0f;
+      rem = a.max_depth;
+      last = -1;
+      fresh = false;
+    }
+
+    // ---- one ray-color level: hit-anything over all bodies ----
+    --rem;
+    ++segs;
+    const float len = sqrtf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
+    const float ux = dx / len, uy = dy / len, uz = dz / len;   // vec3a/unit
+    const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
+    float best_t = INFINITY;
+    int best = -1;
+#pragma unroll 4
+    for (int s = 0; s < n; ++s) {
+      float4 g;
+      if constexpr (SRC == SRC_LDS) g = s_geo[s];
+      else g = a.geo[s];
+      // hittable.clj:10-14 with a unit direction: a = 1, h = u.oc,
+      // c = |oc|^2 - r^2 (y first: the big ground sphere cancels exactly in the fma)
+      const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
+      const float h = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
+      const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
+      const float disc = fmaf(h, h, -c);
+      // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
+      if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) {
+        // the body the ray is leaving: exact arithmetic has c = 0 there
+        // (origin on its surface), so sq = |h| (self-hit acne guard)
+        const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
+        float t = h - sq;                 // nearer root (:15)
+        if (!(t > tmin)) t = h + sq;      // farther root (:16-18)
+        if (t > tmin && t < best_t) {     // open interval, strictly closer (:19, :35-42)
+          best_t = t;
+          best = s;
+        }
+      }
+    }
+
+    bool done = false;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    if (best < 0) {
+      // sky (raytracing.clj:55-58)
+      const float sa = 0.5f * (uy + 1.0f);
+      const float om = 1.0f - sa;
+      cr = tr * fmaf(sa, 0.5f, om);
+      cg = tg * fmaf(sa, 0.7f, om);
+      cb = tb * fmaf(sa, 1.0f, om);
+      done = true;
+    } else if (rem == 0) {
+      done = true;  // the scattered ray would get depth 0 -> black (:46-47)
+    } else {
+      // ---- hit record (hittable.clj:24-31, ray.clj:7-8, hit.clj:14-15) ----
+      const float4 sp = a.sph[best];
+      const float hx = fmaf(ux, best_t, ox);
+      const float hy = fmaf(uy, best_t, oy);
+      const float hz = fmaf(uz, best_t, oz);
+      float nx = (hx - sp.x) / sp.w, ny = (hy - sp.y) / sp.w, nz = (hz - sp.z) / sp.w;
+      const bool front = fmaf(dz, nz, fmaf(dy, ny, dx * nx)) < 0.0f;
+      if (!front) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+      }
+      const int kind = a.kind[best];
+      const float4 m = a.mat[best];
+      ox = hx;
+      oy = hy;
+      oz = hz;
+      last = best;
+      if (kind == RT_LAMBERTIAN) {
+        // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
+        float rx, ry, rz;
+        random_unit(st, rx, ry, rz);
+        float sx = rx + nx, sy = ry + ny, sz = rz + nz;
+        if (fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {
+          sx = nx;
+          sy = ny;
+          sz = nz;
+        }
+        dx = sx;
+        dy = sy;
+        dz = sz;
+        tr *= m.x;
+        tg *= m.y;
+        tb *= m.z;
+      } else if (kind == RT_METAL) {
+        // material.clj:21-28: reflect the *un-normalised* d, add fuzz*unit
+        const float k2 = 2.0f * fmaf(dz, nz, fmaf(dy, ny, dx * nx));
+        const float rx0 = fmaf(-nx, k2, dx), ry0 = fmaf(-ny, k2, dy), rz0 = fmaf(-nz, k2, dz);
+        float qx, qy, qz;
+        random_unit(st, qx, qy, qz);
+        const float rx = fmaf(m.w, qx, rx0), ry = fmaf(m.w, qy, ry0), rz = fmaf(m.w, qz, rz0);
+        if (fmaf(rz, nz, fmaf(ry, ny, rx * nx)) > 0.0f) {
+          dx = rx;
+          dy = ry;
+          dz = rz;
+          tr *= m.x;
+          tg *= m.y;
+          tb *= m.z;
+        } else {
+          done = true;  // absorbed: scatter-fn nil -> black (:51-54)
+        }
+      } else if (kind == RT_NONE) {
+        done = true;  // no ::scatter-fn -> black (raytracing.clj:49-54)
+      } else {
+        // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
+        const float ri = front ? (1.0f / m.w) : m.w;
+        const float un = fmaf(uz, nz, fmaf(uy, ny, ux * nx));
+        const float cosv = fminf(-un, 1.0f);
+        const float sinv = sqrtf(fmaf(-cosv, cosv, 1.0f));
+        bool refl = !(ri * sinv <= 1.0f);
+        if (!refl) {
+          const float xi = rng_uniform(st);  // drawn only when refraction is possible
+          float r0 = (1.0f - ri) / (1.0f + ri);
+          r0 = r0 * r0;
+          const float x1 = 1.0f - cosv;
+          const float x2 = x1 * x1;
+          const float x5 = x2 * x2 * x1;
+          refl = fmaf(1.0f - r0, x5, r0) > xi;
+        }
+        if (refl) {
+          const float k2 = 2.0f * un;
+          dx = fmaf(-nx, k2, ux);
+          dy = fmaf(-ny, k2, uy);
+          dz = fmaf(-nz, k2, uz);
+        } else {
+          const float qx = fmaf(nx, cosv, ux) * ri;
+          const float qy = fmaf(ny, cosv, uy) * ri;
+          const float qz = fmaf(nz, cosv, uz) * ri;
+          const float par = -sqrtf(fabsf(1.0f - fmaf(qz, qz, fmaf(qy, qy, qx * qx))));
+          dx = fmaf(nx, par, qx);
+          dy = fmaf(ny, par, qy);
+          dz = fmaf(nz, par, qz);
+        }
+      }
+    }
+
+    if (done) {
+      accr += cr;
+      accg += cg;
+      accb += cb;
+      fresh = true;
+      if (++k >= a.spp) active = false;
+    }
+  }
+
+  if (px < a.width && ro < a.rows_out) {
+    const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
+    float* o = a.out + (static_cast<size_t>(ro) * a.width + px) * 3;
+    o[0] = accr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
+    o[1] = accg / inv;
+    o[2] = accb / inv;
+  }
+
+  if (a.counters) {
+    // one 64-bit atomic per wave: segments and samples of its 64 lanes
+    uint32_t v = segs;
+    uint32_t smp = (px < a.width && ro < a.rows_out && a.max_depth > 0 && a.spp > 0)
+                       ? static_cast<uint32_t>(a.spp) : 0u;
+    for (int off = 32; off > 0; off >>= 1) {
+      v += __shfl_xor(v, off);
+      smp += __shfl_xor(smp, off);
+    }
+    if (lane == 0) {
+      atomicAdd(&a.counters[0], static_cast<unsigned long long>(v));
+      atomicAdd(&a.counters[1], static_cast<unsigned long long>(smp));
+    }
+  }
+}
+
+// ------------------------------------------------------------- host ------
+static int g_variant = 0;  // 0 default (= LDS), 1 LDS, 2 scalar
+
+}  // namespace rtclj
+
+using namespace rtclj;
+
+struct rt_dscene {
+  int device;
+  int n;
+  float4* geo;
+  float4* sph;
+  float4* mat;
+  int* kind;
+};
+
+static int hip_fail(hipError_t e, const char* what) {
+  return set_error(RT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(call)                                  \
+  do {                                                 \
+    hipError_t _e = (call);                            \
+    if (_e != hipSuccess) return hip_fail(_e, #call);  \
+  } while (0)
+
+extern "C" int rt_set_variant(int v) {
+  const int old = g_variant;
+  if (v >= 0 && v <= 2) g_variant = v;
+  return old;
+}
+
+extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
+  clear_error();
+  if (!s || !out) return set_error(RT_E_ARG, "rt_scene_upload: NULL argument");
+  *out = nullptr;
+  if (s->n < 0 || (s->n > 0 && (!s->sphere || !s->mat_kind || !s->mat)))
+    return set_error(RT_E_ARG, "rt_scene_upload: bad scene arrays");
+  if (s->n > RT_MAX_SPHERES)
+    return set_error(RT_E_TOO_MANY, "rt_scene_upload: " + std::to_string(s->n) +
+                                        " spheres > RT_MAX_SPHERES (" +
+                                        std::to_string(RT_MAX_SPHERES) + ")");
+  for (int i = 0; i < s->n; ++i) {
+    const int k = s->mat_kind[i];
+    if (k != RT_LAMBERTIAN && k != RT_METAL && k != RT_DIELECTRIC && k != RT_NONE)
+      return set_error(RT_E_MATERIAL, "rt_scene_upload: body " + std::to_string(i) +
+                                          " has unsupported material kind " + std::to_string(k));
+  }
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return set_error(RT_E_NODEV, "rt_scene_upload: device " + std::to_string(device) +
+                                     " not available (" + std::to_string(ndev) + " visible)");
+  HIP_TRY(hipSetDevice(device));
+  const int n = s->n;
+  const size_t cnt = n > 0 ? n : 1;
+  std::vector<float4> geo(cnt), sph(cnt), mat(cnt);
+  std::vector<int> kind(cnt, 0);
+  for (int i = 0; i < n; ++i) {
+    const float* q = s->sphere + 4 * i;
+    const float r = q[3];
+    geo[i] = make_float4(q[0], q[1], q[2], -(r * r));
+    sph[i] = make_float4(q[0], q[1], q[2], r);
+    const float* m = s->mat + 4 * i;
+    mat[i] = make_float4(m[0], m[1], m[2], m[3]);
+    kind[i] = s->mat_kind[i];
+  }
+  rt_dscene* d = new rt_dscene{device, n, nullptr, nullptr, nullptr, nullptr};
+  hipError_t e = hipMalloc(&d->geo, cnt * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&d->sph, cnt * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&d->mat, cnt * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&d->kind, cnt * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpy(d->geo, geo.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d->sph, sph.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d->mat, mat.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d->kind, kind.data(), cnt * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    rt_scene_free(d);
+    return hip_fail(e, "rt_scene_upload");
+  }
+  *out = d;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_free(rt_dscene* d) {
+  if (!d) return RT_OK;
+  (void)hipSetDevice(d->device);
+  if (d->geo) (void)hipFree(d->geo);
+  if (d->sph) (void)hipFree(d->sph);
+  if (d->mat) (void)hipFree(d->mat);
+  if (d->kind) hipFree(d->kind);
+  delete d;
+  return RT_OK;
+}
+
+extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p, float* d_out,
+                         uint64_t* d_counters, void* hip_stream) {
+  clear_error();
+  if (!ds || !c || !p || !d_out) return set_error(RT_E_ARG, "rt_launch: NULL argument");
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->flags != 0)
+    return set_error(RT_E_ARG, "rt_launch: bad width/height/spp/flags");
+  const int rows = rows_out(*p);
+  if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
+  KArgs a{};
+  a.geo = ds->geo;
+  a.sph = ds->sph;
+  a.mat = ds->mat;
+  a.kind = ds->kind;
+  a.out = d_out;
+  a.counters = reinterpret_cast<unsigned long long*>(d_counters);
+  std::memcpy(a.cam + 0, c->center, 12);
+  std::memcpy(a.cam + 3, c->p00, 12);
+  std::memcpy(a.cam + 6, c->du, 12);
+  std::memcpy(a.cam + 9, c->dv, 12);
+  std::memcpy(a.cam + 12, c->disk_u, 12);
+  std::memcpy(a.cam + 15, c->disk_v, 12);
+  a.defocus = c->defocus ? 1 : 0;
+  a.n = ds->n;
+  a.width = p->width;
+  a.rows_out = rows;
+  a.row_begin = p->row_begin;
+  a.row_tile = p->row_tile > 0 ? p->row_tile : 8;
+  a.tile_first = p->tile_first;
+  a.tile_step = p->tile_step;
+  a.spp = p->spp;
+  a.sample_begin = p->sample_begin;
+  a.max_depth = p->max_depth;
+  a.key = seed_key(p->seed);
+  if (rows == 0) return RT_OK;
+  HIP_TRY(hipSetDevice(ds->device));
+  const dim3 grid((p->width + 15) / 16, (rows + 15) / 16);
+  const dim3 block(256);
+  hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  if (g_variant == 2) {
+    hipLaunchKernelGGL(trace_kernel<SRC_SCALAR>, grid, block, 0, stream, a);
+  } else {
+    const size_t lds = static_cast<size_t>(ds->n > 0 ? ds->n : 1) * sizeof(float4);
+    static bool attr_set[64] = {};
+    if (ds->device < 64 && !attr_set[ds->device]) {
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<SRC_LDS>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  RT_MAX_SPHERES * static_cast<int>(sizeof(float4))));
+      attr_set[ds->device] = true;
+    }
+    hipLaunchKernelGGL(trace_kernel<SRC_LDS>, grid, block, lds, stream, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
