@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py — Mray-samples/s of the MI355X trace kernel on BASELINE.json's C1.
+
+Workload (BASELINE.json configs[1], the metric's own config): the RTIOW cover
+scene (grid 11 -> 484 bodies, generator seed 42) at 1200x675, 100 spp,
+depth 50, fp32, render seed 1.  A "step" renders one full frame's share:
+
+  * --scaling weak (default): every rank renders the whole 1200x675 frame
+    with its own 100-sample stripe (samples [100*rank, 100*rank+100)), so
+    per-GPU work is fixed; ranks share nothing (no collective on the data
+    path; the RNG is keyed by (seed, pixel, sample)).
+  * --scaling strong: the single 100-spp frame is split into interleaved
+    8-row tiles, tile t on rank t % N (the north_star row-tile shard).
+
+Inputs (scene table, camera) are resident in HBM before timing; the frame
+stays on the device (host gather is not in `value`).  Timing: W untimed
+warm-up steps, then K steps bracketed by barrier + synchronize, max over
+ranks; kernel duration from HIP events on the launch stream.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "raytracing-clj_amd"))
+
+import torch  # noqa: E402  (first: librtclj.so then binds to torch's HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import rtclj  # noqa: E402
+from rtclj import scenes  # noqa: E402
+from rtclj._lib import check, lib, rt_params  # noqa: E402
+
+METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
+FLOPS_PER_SEGMENT = 100    # per-segment hit/scatter/sky work (nominal)
+
+WORKLOADS = {
+    "c1": dict(width=1200, spp=100, depth=50, grid=11, name="C1 RTIOW cover 1200x675 100spp depth50"),
+    "c2": dict(width=3840, spp=500, depth=50, grid=11, name="C2 cover 3840x2160 500spp depth50"),
+    "c4": dict(width=7680, spp=2000, depth=64, grid=16, name="C4 cover(1025) 7680x4320 2000spp depth64"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
+    ap.add_argument("--spp", type=int, default=None, help="override the workload's spp (not a bench line)")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
+    """The oracle's fp64 reference-semantics mode (the C++ restatement of the
+    Clojure path) on a bounded row sample of the same frame, on host cores."""
+    sys.path.insert(0, str(ROOT))
+    import numpy as np
+    import oracle
+    nthreads = max(1, min(threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    _, _, segs, samples = oracle.render(oracle.MODE_REF64, scene.sphere.astype(np.float64), scene.kind,
+                                        scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
+                                        seed=seed, row_step=row_step, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    rows = (h + row_step - 1) // row_step
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": samples / dt / 1e6, "unit": "Mray-samples/s", "cores": nthreads, "kind": "port",
+            "sample": f"rows 0,{row_step},{2 * row_step},... ({rows} rows x {w} px x {spp} spp = {samples} samples) "
+                      f"of the same frame, fp64 reference semantics (oracle MODE_REF64), {dt:.1f} s",
+            "seconds": dt, "segments_per_sample": segs / max(samples, 1), "cpu_model": cpu,
+            "host": platform.node()}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.gpus > 1 and world == 1:
+        raise SystemExit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
+    if not torch.cuda.is_available() or lib.rt_device_count() <= 0:
+        raise SystemExit("bench.py needs a GPU (MI355X); no device visible")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(backend=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
+    lib.rt_set_variant(a.variant)
+
+    wl = dict(WORKLOADS[a.workload])
+    if a.spp:
+        wl["spp"] = a.spp
+    W = wl["width"]
+    H = rtclj.raytracing.image_height(W)
+    spp, depth = wl["spp"], wl["depth"]
+    scene = scenes.cover(wl["grid"], 42)
+    cam = scenes.cover_camera(W, H)
+
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(local, C.byref(scene.c), C.byref(ds)))
+    if a.scaling == "weak":
+        p = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
+                      sample_begin=rank * spp)
+    else:
+        p = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
+                      row_tile=8, tile_first=rank, tile_step=world if world > 1 else 0)
+    rows = check(lib.rt_rows_out(C.byref(p)))
+    out = torch.empty(rows * W * 3, dtype=torch.float32, device=dev)
+    counters = torch.zeros(2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+
+    def step():
+        check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()),
+                            C.c_void_p(counters.data_ptr()), sh))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    counters.zero_()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        starts[k].record(stream)
+        step()
+        ends[k].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    cnt = counters.to("cpu").tolist()
+    local_stats = torch.tensor([elapsed, max(kern_ms), sum(kern_ms) / len(kern_ms)], dtype=torch.float64)
+    tot = torch.tensor([float(cnt[0]), float(cnt[1])], dtype=torch.float64)
+    if world > 1:
+        ls, tt = local_stats.to(dev), tot.to(dev)
+        dist.all_reduce(ls, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        local_stats, tot = ls.cpu(), tt.cpu()
+    elapsed, kern_max_ms, kern_avg_ms = local_stats.tolist()
+    segs_total, samples_total = tot.tolist()
+    lib.rt_scene_free(ds)
+
+    if rank == 0:
+        samples_per_step = samples_total / a.steps
+        value = samples_per_step * a.steps / elapsed / 1e6
+        seg_per_sample = segs_total / max(samples_total, 1)
+        # dominant kernel, per launch on this rank (rank-0 share at N>1)
+        launch_samples = rows * W * spp
+        launch_segs = seg_per_sample * launch_samples
+        flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT)
+        tflops = flops / (kern_avg_ms * 1e-3) / 1e12
+        hbm_bytes = rows * W * 12 + len(scene) * 32
+        gbs = hbm_bytes / (kern_avg_ms * 1e-3) / 1e9
+        res = {
+            "metric": METRIC, "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "fp32",
+            "data": f"synthetic: RTIOW cover scene (grid {wl['grid']}, {len(scene)} bodies, generator seed 42), "
+                    f"render seed {a.seed}",
+            "config": {"workload": wl["name"] if not a.spp else f"{wl['name']} (spp override {spp})",
+                       "width": W, "height": H, "spp_per_gpu": spp, "max_depth": depth, "bodies": len(scene),
+                       "parallelism": ("sample-stripe x%d (weak)" % world) if a.scaling == "weak"
+                       else ("row-tile 8 x%d (strong)" % world), "variant": a.variant},
+            "roofline": {"bound": "valu", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tflops / PEAK_FP32_TFLOPS, "traffic": None,
+                         "note": f"fp32 VALU (no MFMA: branchy scalar FP). algorithmic flops/launch = segments "
+                                 f"x (17 x {len(scene)} bodies + 100); peak = fp32 vector peak"},
+            "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+                             "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
+            "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
+            "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
+            "kernel": "rtclj::trace_kernel<%d>" % (2 if a.variant == 2 else 1),
+            "cpu_baseline": None,
+        }
+        if a.cpu_baseline == "auto" and world == 1:
+            res["cpu_baseline"] = cpu_baseline(scene, cam, W, H, spp, depth, a.seed, a.cpu_row_step, a.cpu_threads)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

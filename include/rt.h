@@ -94,8 +94,13 @@ typedef struct rt_params {
   int row_tile;           /* interleaved tile height (rows); 0 -> 8            */
   int tile_first;         /* rt_launch: first tile of this shard               */
   int tile_step;          /* rt_launch: tile stride (0 = contiguous rows)      */
-  int flags;              /* reserved, must be 0                               */
+  int flags;              /* 0, or RT_FLAG_SHARDS_ON_DEVICE0                   */
 } rt_params;
+
+/* rt_render: split into n_devices interleaved-tile shards exactly as for n
+ * GPUs, but run every shard on device 0 (exercises the multi-GPU fan-out and
+ * host gather on a one-GPU machine).  n_devices must be > 0. */
+#define RT_FLAG_SHARDS_ON_DEVICE0 1
 
 /* ---- per-call statistics (device-side counters) ------------------------- */
 typedef struct rt_stats {

@@ -34,7 +34,7 @@ def _lib():
         dp, ip, fp, u64p = C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_float), C.POINTER(C.c_uint64)
         d.oracle_render.restype = C.c_int
         d.oracle_render.argtypes = [C.c_int, C.c_int, dp, ip, dp, dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                    C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, fp, dp, u64p]
+                                    C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, fp, dp, u64p]
         d.oracle_sphere_hit.restype = C.c_int
         d.oracle_sphere_hit.argtypes = [dp, dp, dp, C.c_double, C.c_double, dp]
         d.oracle_reflect.argtypes = [dp, dp, dp]
@@ -55,18 +55,20 @@ def _d(a):
 
 
 def render(mode, sphere, kind, mat, cam, defocus, width, height, spp, max_depth, seed=1, rows=None,
-           sample_begin=0, nthreads=0, want64=False):
-    """Render rows [r0,r1) -> (float32 (rows,W,3), float64 or None, segments, samples)."""
+           sample_begin=0, nthreads=0, want64=False, row_step=1):
+    """Render rows r0, r0+row_step, ... < r1 (default all) -> (float32 (rows,W,3),
+    float64 or None, segments, samples)."""
     r0, r1 = (0, height) if rows is None else rows
+    nrows = (r1 - r0 + row_step - 1) // row_step
     sph, sp = _d(np.asarray(sphere, np.float64).reshape(-1, 4))
     mt, mp = _d(np.asarray(mat, np.float64).reshape(-1, 4))
     kd = np.ascontiguousarray(kind, np.int32).reshape(-1)
     cm, cp = _d(np.asarray(cam, np.float64).reshape(18))
-    out = np.empty((r1 - r0, width, 3), np.float32)
-    out64 = np.empty((r1 - r0, width, 3), np.float64) if want64 else None
+    out = np.empty((nrows, width, 3), np.float32)
+    out64 = np.empty((nrows, width, 3), np.float64) if want64 else None
     cnt = np.zeros(2, np.uint64)
     rc = _lib().oracle_render(mode, len(kd), sp, kd.ctypes.data_as(C.POINTER(C.c_int)), mp, cp, int(defocus),
-                              width, height, r0, r1, spp, sample_begin, max_depth, seed, nthreads,
+                              width, height, r0, r1, row_step, spp, sample_begin, max_depth, seed, nthreads,
                               out.ctypes.data_as(C.POINTER(C.c_float)),
                               out64.ctypes.data_as(C.POINTER(C.c_double)) if want64 else None,
                               cnt.ctypes.data_as(C.POINTER(C.c_uint64)))

@@ -396,15 +396,15 @@ struct Job {
   double cam64[18];
   float cam32[18];
   bool defocus;
-  int width, row_begin, spp, sample_begin, max_depth;
+  int width, row_begin, row_step, spp, sample_begin, max_depth;
   uint32_t key;
   float* out;
   double* out64;
 };
 
-void render_row(const Job& J, int ro, uint64_t* segs) {
-  const int gy = J.row_begin + ro;
-  for (int px = 0; px < J.width; ++px) {
+void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
+  const int gy = J.row_begin + ro * J.row_step;
+  for (int px = x0; px < x1; ++px) {
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(J.width) + static_cast<uint32_t>(px);
     const size_t o = (static_cast<size_t>(ro) * J.width + px) * 3;
     if (J.mode == MODE_REF64) {
@@ -460,15 +460,17 @@ void render_row(const Job& J, int ro, uint64_t* segs) {
 
 extern "C" {
 
-// Render rows [row_begin, row_end) into out (rows x width x 3 fp32, and
+// Render rows row_begin, row_begin+row_step, ... < row_end into out
+// (compacted: rows x width x 3 fp32, and
 // optionally out64 in double for MODE_REF64).  sphere/mat: n x 4 doubles,
 // cam: 18 doubles (center, p00, du, dv, disk_u, disk_v).  nthreads <= 0 ->
 // hardware concurrency.  counters (nullable): [segments, samples].
 int oracle_render(int mode, int n, const double* sphere, const int* kind, const double* mat,
                   const double* cam, int defocus, int width, int height, int row_begin, int row_end,
-                  int spp, int sample_begin, int max_depth, uint64_t seed, int nthreads, float* out,
-                  double* out64, uint64_t* counters) {
+                  int row_step, int spp, int sample_begin, int max_depth, uint64_t seed, int nthreads,
+                  float* out, double* out64, uint64_t* counters) {
   if (width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_end < row_begin || !out ||
+      row_step <= 0 ||
       (n > 0 && (!sphere || !kind || !mat)) || !cam || (mode != MODE_REF64 && mode != MODE_MIRROR32))
     return -1;
   Job J{};
@@ -496,13 +498,14 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
   J.defocus = defocus != 0;
   J.width = width;
   J.row_begin = row_begin;
+  J.row_step = row_step;
   J.spp = spp;
   J.sample_begin = sample_begin;
   J.max_depth = max_depth;
   J.key = seed_key(seed);
   J.out = out;
   J.out64 = out64;
-  const int rows = row_end - row_begin;
+  const int rows = (row_end - row_begin + row_step - 1) / row_step;  // rows r0, r0+step, ... < r1
   if (spp <= 0 || max_depth <= 0) {
     // depth <= 0 -> black (raytracing.clj:46-47); spp 0 -> 0/0 in the
     // reference, defined here (and on the GPU) as 0/1 = black.
@@ -511,12 +514,19 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
     if (counters) counters[0] = counters[1] = 0;
     return 0;
   }
+  // work items: 32-pixel row chunks, handed out by an atomic counter
+  constexpr int CH = 32;
+  const int per_row = (width + CH - 1) / CH;
+  const int items = rows * per_row;
   int nt = nthreads > 0 ? nthreads : static_cast<int>(std::thread::hardware_concurrency());
-  nt = std::max(1, std::min(nt, std::max(rows, 1)));
+  nt = std::max(1, std::min(nt, std::max(items, 1)));
   std::atomic<int> next{0};
   std::vector<uint64_t> segs(nt, 0);
   auto work = [&](int tid) {
-    for (int r; (r = next.fetch_add(1)) < rows;) render_row(J, r, &segs[tid]);
+    for (int it; (it = next.fetch_add(1)) < items;) {
+      const int r = it / per_row, x0 = (it % per_row) * CH;
+      render_row(J, r, x0, std::min(width, x0 + CH), &segs[tid]);
+    }
   };
   if (nt == 1) {
     work(0);

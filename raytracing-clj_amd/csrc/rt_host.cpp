@@ -222,7 +222,9 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   clear_error();
   const auto t0 = std::chrono::steady_clock::now();
   if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, "rt_render: NULL argument");
-  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->flags != 0 || p->n_devices < 0)
+  const bool on_dev0 = p->flags == RT_FLAG_SHARDS_ON_DEVICE0;
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->n_devices < 0 ||
+      (p->flags != 0 && !on_dev0) || (on_dev0 && p->n_devices == 0))
     return set_error(RT_E_ARG, "rt_render: bad width/height/spp/flags/n_devices");
   if (p->tile_step != 0 || p->tile_first != 0)
     return set_error(RT_E_ARG, "rt_render: tile_first/tile_step are per-shard (rt_launch) fields");
@@ -234,7 +236,7 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   const int ndev_vis = rt_device_count();
   if (ndev_vis <= 0) return set_error(RT_E_NODEV, "rt_render: no GPU visible");
   int ndev = p->n_devices == 0 ? ndev_vis : p->n_devices;
-  if (ndev > ndev_vis)
+  if (ndev > ndev_vis && !on_dev0)
     return set_error(RT_E_NODEV, "rt_render: n_devices " + std::to_string(ndev) + " > visible " +
                                      std::to_string(ndev_vis));
   const int T = p->row_tile > 0 ? p->row_tile : 8;
@@ -244,8 +246,9 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   std::vector<Shard> shards(ndev);
   for (int d = 0; d < ndev; ++d) {
     Shard& sh = shards[d];
-    sh.device = d;
+    sh.device = on_dev0 ? 0 : d;
     sh.p = *p;
+    sh.p.flags = 0;
     sh.p.row_tile = T;
     if (ndev > 1) {
       sh.p.tile_first = d;

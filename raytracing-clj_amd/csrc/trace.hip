@@ -421,7 +421,7 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   if (d->geo) (void)hipFree(d->geo);
   if (d->sph) (void)hipFree(d->sph);
   if (d->mat) (void)hipFree(d->mat);
-  if (d->kind) hipFree(d->kind);
+  if (d->kind) (void)hipFree(d->kind);
   delete d;
   return RT_OK;
 }

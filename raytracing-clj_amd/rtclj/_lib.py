@@ -16,6 +16,7 @@ library_path = _PKG_ROOT / "lib" / "librtclj.so"
 RT_OK, RT_E_ARG, RT_E_MATERIAL, RT_E_TOO_MANY, RT_E_HIP, RT_E_NODEV, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_NONE = 0, 1, 2, 3
 RT_MAX_SPHERES = 8192
+RT_FLAG_SHARDS_ON_DEVICE0 = 1
 
 
 class RTError(RuntimeError):

@@ -119,7 +119,8 @@ def camera(image_width, image_h, vfov, look_from, look_at, vup, defocus_angle, f
 
 
 def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50, seed: int = 1,
-           n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None):
+           n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None,
+           flags: int = 0):
     """compute-pixel for every pixel of rows [r0, r1) (default: all), on the GPU.
 
     Returns float32 (rows, width, 3) linear RGB, each pixel the mean of its spp
@@ -128,7 +129,7 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
         scene = Scene.from_bodies(scene)
     r0, r1 = (0, height) if rows is None else rows
     p = rt_params(width=width, height=height, row_begin=r0, row_end=r1, spp=spp, max_depth=max_depth,
-                  seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile)
+                  seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
     out = np.empty((max(r1 - r0, 0), width, 3), np.float32)
     st = rt_stats()
     check(lib.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st)))

@@ -1,0 +1,23 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+for p in (ROOT, ROOT / "raytracing-clj_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def gpu_lib():
+    """The product library with at least one visible GPU (fails loudly otherwise)."""
+    import rtclj
+
+    n = rtclj.lib.rt_device_count()
+    assert n > 0, "no GPU visible to librtclj.so (HIP); GPU tests must run on the MI355X box"
+    return rtclj
