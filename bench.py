@@ -41,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 import rtclj  # noqa: E402
 from rtclj import scenes  # noqa: E402
 from rtclj._lib import check, lib, rt_params  # noqa: E402
+from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
 METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
@@ -127,13 +128,9 @@ def main():
 
     ds = C.c_void_p()
     check(lib.rt_scene_upload(local, C.byref(scene.c), C.byref(ds)))
-    if a.scaling == "weak":
-        p = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
-                      sample_begin=rank * spp)
-    else:
-        p = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
-                      row_tile=8, tile_first=rank, tile_step=world if world > 1 else 0)
+    p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
     rows = check(lib.rt_rows_out(C.byref(p)))
+    assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
     out = torch.empty(rows * W * 3, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)

@@ -15,7 +15,7 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "_build" / "liboracle.so"
-MODE_REF64, MODE_MIRROR32 = 0, 1
+MODE_REF64, MODE_MIRROR32, MODE_BOOK64 = 0, 1, 2
 
 _dll = None
 
@@ -44,6 +44,11 @@ def _lib():
         d.oracle_quantize.restype = C.c_int
         d.oracle_quantize.argtypes = [C.c_double]
         d.oracle_camera.argtypes = [C.c_int, C.c_int, C.c_double, dp, dp, dp, C.c_double, C.c_double, dp]
+        d.oracle_lambertian_dir.argtypes = [dp, dp, dp]
+        d.oracle_metal_dir.restype = C.c_int
+        d.oracle_metal_dir.argtypes = [dp, dp, C.c_double, dp, dp]
+        d.oracle_dielectric_dir.restype = C.c_int
+        d.oracle_dielectric_dir.argtypes = [dp, dp, C.c_int, C.c_double, C.c_double, dp]
         d.oracle_rng_stream.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, fp]
         _dll = d
     return _dll
@@ -123,3 +128,28 @@ def rng_stream(seed, pixel, sample, n):
     out = np.zeros(n, np.float32)
     _lib().oracle_rng_stream(seed, pixel, sample, n, out.ctypes.data_as(C.POINTER(C.c_float)))
     return out
+
+
+def lambertian_dir(unit, n):
+    a, ap = _d(unit)
+    b, bp = _d(n)
+    o, op = _d(np.zeros(3))
+    _lib().oracle_lambertian_dir(ap, bp, op)
+    return o.tolist()
+
+
+def metal_dir(d, n, fuzz, unit):
+    a, ap = _d(d)
+    b, bp = _d(n)
+    u, up = _d(unit)
+    o, op = _d(np.zeros(3))
+    ok = _lib().oracle_metal_dir(ap, bp, fuzz, up, op)
+    return bool(ok), o.tolist()
+
+
+def dielectric_dir(d, n, front, eta, xi):
+    a, ap = _d(d)
+    b, bp = _d(n)
+    o, op = _d(np.zeros(3))
+    refl = _lib().oracle_dielectric_dir(ap, bp, int(front), eta, xi, op)
+    return bool(refl), o.tolist()

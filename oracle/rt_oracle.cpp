@@ -42,7 +42,11 @@
 
 namespace {
 
-enum { MODE_REF64 = 0, MODE_MIRROR32 = 1 };
+enum { MODE_REF64 = 0, MODE_MIRROR32 = 1, MODE_BOOK64 = 2 };
+
+// MODE_BOOK64: MODE_REF64 but metal reflects unit(d) as the RTIOW book does
+// (negative control: scene.ppm must reject it).
+thread_local bool t_book_metal = false;
 enum { LAMB = 0, METAL = 1, DIEL = 2, NONE = 3 };
 
 // ------------------------------------------------------------ RNG (contract)
@@ -193,7 +197,7 @@ V ray_color64(const Scene64& sc, V o, V d, int depth, Rng& rng, uint64_t* segs) 
         break;
       }
       case METAL: {  // material.clj:21-28
-        const V refl = reflect64(d, h.n);
+        const V refl = reflect64(t_book_metal ? vunit(d) : d, h.n);
         const V r2 = vadd(vmul(random_unit64(rng), m[3]), refl);
         if (!(vdot(r2, h.n) > 0)) return V{0, 0, 0};
         sd = r2;
@@ -404,10 +408,11 @@ struct Job {
 
 void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
   const int gy = J.row_begin + ro * J.row_step;
+  t_book_metal = J.mode == MODE_BOOK64;
   for (int px = x0; px < x1; ++px) {
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(J.width) + static_cast<uint32_t>(px);
     const size_t o = (static_cast<size_t>(ro) * J.width + px) * 3;
-    if (J.mode == MODE_REF64) {
+    if (J.mode == MODE_REF64 || J.mode == MODE_BOOK64) {
       // compute-pixel (raytracing.clj:141-155)
       const double* c = J.cam64;
       const V center{c[0], c[1], c[2]}, p00{c[3], c[4], c[5]}, du{c[6], c[7], c[8]}, dv{c[9], c[10], c[11]};
@@ -471,7 +476,7 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
                   float* out, double* out64, uint64_t* counters) {
   if (width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_end < row_begin || !out ||
       row_step <= 0 ||
-      (n > 0 && (!sphere || !kind || !mat)) || !cam || (mode != MODE_REF64 && mode != MODE_MIRROR32))
+      (n > 0 && (!sphere || !kind || !mat)) || !cam || mode < MODE_REF64 || mode > MODE_BOOK64)
     return -1;
   Job J{};
   J.mode = mode;
@@ -578,6 +583,40 @@ void oracle_refract(const double* uv, const double* n, double eta, double* out) 
 }
 
 double oracle_reflectance(double cosine, double ri) { return reflectance64(cosine, ri); }
+
+// material scatter directions with the random draws injected (material.clj):
+// lambertian: unit + n, n if near-zero (:13-19, vec3a.clj:88-92)
+void oracle_lambertian_dir(const double* unit, const double* n, double* out) {
+  const V nn{n[0], n[1], n[2]};
+  const V s = vadd(V{unit[0], unit[1], unit[2]}, nn);
+  const V r = near_zero64(s) ? nn : s;
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
+}
+// metal (:21-28): returns 1 if scattered (dot > 0), 0 if absorbed
+int oracle_metal_dir(const double* d, const double* n, double fuzz, const double* unit, double* out) {
+  const V nn{n[0], n[1], n[2]};
+  const V r = vadd(vmul(V{unit[0], unit[1], unit[2]}, fuzz), reflect64(V{d[0], d[1], d[2]}, nn));
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
+  return vdot(r, nn) > 0 ? 1 : 0;
+}
+// dielectric (:34-46) with the uniform draw xi; returns 1 reflected, 0 refracted
+int oracle_dielectric_dir(const double* d, const double* n, int front, double eta, double xi, double* out) {
+  const V nn{n[0], n[1], n[2]};
+  const double ri = front ? (1.0 / eta) : eta;
+  const V u = vunit(V{d[0], d[1], d[2]});
+  const double cs = std::min(vdot(vneg(u), nn), 1.0);
+  const double sn = std::sqrt(1.0 - cs * cs);
+  const bool refl = !(ri * sn <= 1.0) || reflectance64(cs, ri) > xi;
+  const V r = refl ? reflect64(u, nn) : refract64(u, nn, ri);
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
+  return refl ? 1 : 0;
+}
 
 // write-color! (raytracing.clj:19-26) for one channel
 int oracle_quantize(double c) {

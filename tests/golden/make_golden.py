@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Regenerate the committed golden fixtures (run in the build container,
+where /root/reference exists; nothing at test time reads /root/reference).
+
+  scene_ppm.npz          the reference's only hot-path output, scene.ppm
+                         (400x225 P3, `clojure -M:main` = 100 spp, depth 50),
+                         as uint8 pixels (data, not source)
+  scene_ppm_stats.json   its whole-image mean, 16x9 block means,
+                         neighbour-difference std (SURVEY.md §8c definitions)
+  kats.json              known answers for the hot-path functions, computed
+                         here by a pure-Python fp64 restatement of the Clojure
+                         formulas (independent of oracle/rt_oracle.cpp)
+  rng_golden.json        the keyed RNG contract (lowbias32 + xorshift32),
+                         computed here in pure Python
+  mirror_small.npz       small renders by the oracle's fp32 kernel mirror
+                         (regression pins for the oracle and the GPU path)
+
+Usage: python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+REF_PPM = Path("/root/reference/scene.ppm")
+M32 = 0xFFFFFFFF
+
+
+# ---------------------------------------------------------------- scene.ppm
+def read_p3(path):
+    tok = path.read_text().split()
+    assert tok[0] == "P3"
+    w, h, mx = int(tok[1]), int(tok[2]), int(tok[3])
+    assert mx == 255
+    return np.array(tok[4:4 + w * h * 3], np.int64).astype(np.uint8).reshape(h, w, 3)
+
+
+def image_stats(img):
+    """cell (y,x) = mean over rows [y*H//9,(y+1)*H//9), cols
+    [x*W//16,(x+1)*W//16); neighbour diff = img[:,1:] - img[:,:-1]."""
+    img = img.astype(np.float64)
+    h, w = img.shape[:2]
+    blocks = np.array([[img[y * h // 9:(y + 1) * h // 9, x * w // 16:(x + 1) * w // 16].reshape(-1, 3).mean(0)
+                        for x in range(16)] for y in range(9)])
+    return {"mean": img.reshape(-1, 3).mean(0).tolist(), "blocks": blocks.tolist(),
+            "nbr_std": np.diff(img, axis=1).reshape(-1, 3).std(0).tolist(), "width": w, "height": h}
+
+
+# ------------------------------------------------- pure-Python fp64 formulas
+def dot(a, b):
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]
+
+
+def sub(a, b):
+    return [a[0] - b[0], a[1] - b[1], a[2] - b[2]]
+
+
+def add(a, b):
+    return [a[0] + b[0], a[1] + b[1], a[2] + b[2]]
+
+
+def mul(a, s):
+    return [a[0] * s, a[1] * s, a[2] * s]
+
+
+def div(a, s):
+    return [a[0] / s, a[1] / s, a[2] / s]
+
+
+def unit(a):
+    return div(a, math.sqrt(dot(a, a)))
+
+
+def sphere_hit(sph, o, d, tmin, tmax):  # hittable.clj:9-31
+    c, r = sph[:3], sph[3]
+    oc = sub(c, o)
+    a = dot(d, d)
+    h = dot(d, oc)
+    cc = dot(oc, oc) - r * r
+    disc = h * h - a * cc
+    if disc < 0.0:
+        return {"hit": False}
+    sq = math.sqrt(disc)
+    root = (h - sq) / a
+    if root <= tmin or tmax <= root:
+        root = (h + sq) / a
+    if root <= tmin or tmax <= root:
+        return {"hit": False}
+    p = add(o, mul(d, root))
+    out = div(sub(p, c), r)
+    front = dot(d, out) < 0
+    return {"hit": True, "t": root, "p": p, "n": out if front else mul(out, -1.0), "front": front}
+
+
+def reflect(v, n):  # vec3a.clj:94-95
+    return sub(v, mul(n, 2 * dot(v, n)))
+
+
+def refract(uv, n, e):  # vec3a.clj:97-101
+    c = min(dot(mul(uv, -1.0), n), 1.0)
+    perp = mul(add(uv, mul(n, c)), e)
+    par = mul(n, -math.sqrt(abs(1.0 - dot(perp, perp))))
+    return add(perp, par)
+
+
+def reflectance(cosine, ri):  # material.clj:30-32
+    r0 = ((1.0 - ri) / (1.0 + ri)) ** 2
+    return r0 + (1.0 - r0) * (1.0 - cosine) ** 5
+
+
+def quantize(c):  # raytracing.clj:19-26
+    g = math.sqrt(c) if c > 0 else 0.0
+    return int(256 * min(0.999, max(g, 0.0)))
+
+
+def near_zero(v):
+    return all(abs(x) < 1e-8 for x in v)
+
+
+def lambertian_dir(u, n):  # material.clj:13-19
+    s = add(u, n)
+    return n if near_zero(s) else s
+
+
+def metal_dir(d, n, fuzz, u):  # material.clj:21-28
+    r = add(mul(u, fuzz), reflect(d, n))
+    return dot(r, n) > 0, r
+
+
+def dielectric_dir(d, n, front, eta, xi):  # material.clj:34-46
+    ri = (1.0 / eta) if front else eta
+    u = unit(d)
+    cs = min(dot(mul(u, -1.0), n), 1.0)
+    sn = math.sqrt(1.0 - cs * cs)
+    refl = (not (ri * sn <= 1.0)) or reflectance(cs, ri) > xi
+    return refl, (reflect(u, n) if refl else refract(u, n, ri))
+
+
+def camera(w, h, vfov, lf, la, vup, defocus_angle, focus_dist):  # raytracing.clj:105-139
+    theta = (vfov * math.pi) / 180.0
+    hh = math.tan(theta / 2)
+    vh = 2.0 * hh * focus_dist
+    vw = vh * (w / h)
+    W = unit(sub(lf, la))
+    cr = [vup[1] * W[2] - vup[2] * W[1], vup[2] * W[0] - vup[0] * W[2], vup[0] * W[1] - vup[1] * W[0]]
+    U = unit(cr)
+    V = [W[1] * U[2] - W[2] * U[1], W[2] * U[0] - W[0] * U[2], W[0] * U[1] - W[1] * U[0]]
+    vu, vv = mul(U, vw), mul(mul(V, -1.0), vh)
+    du, dv = div(vu, w), div(vv, h)
+    ul = sub(sub(sub(lf, mul(W, focus_dist)), div(vu, 2)), div(vv, 2))
+    p00 = add(ul, mul(add(du, dv), 0.5))
+    rad = focus_dist * math.tan(((defocus_angle / 2.0) * math.pi) / 180.0)
+    return [*lf, *p00, *du, *dv, *mul(U, rad), *mul(V, rad)]
+
+
+# ------------------------------------------------------------ RNG contract
+def mix32(x):
+    x &= M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M32
+    x ^= x >> 16
+    return x
+
+
+def seed_key(seed):
+    return mix32((seed & M32) ^ mix32(((seed >> 32) & M32) ^ 0x85EBCA6B))
+
+
+def stream(seed, pixel, sample, n):
+    pk = mix32(seed_key(seed) ^ mix32(pixel))
+    s = mix32((pk + sample * 0x9E3779B9) & M32) or 0x6D2B79F5
+    out = []
+    for _ in range(n):
+        s ^= (s << 13) & M32
+        s ^= s >> 17
+        s ^= (s << 5) & M32
+        out.append((s >> 8) / 16777216.0)
+    return out
+
+
+def kats():
+    k = {"sphere_hit": [], "reflect": [], "refract": [], "reflectance": [], "quantize": [], "camera": [],
+         "lambertian_dir": [], "metal_dir": [], "dielectric_dir": []}
+    cases = [
+        ("front hit", [0, 0, -1, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, math.inf),
+        ("unnormalised dir", [0, 0, -1, 0.5], [0, 0, 0], [0, 0, -2], 1e-3, math.inf),
+        ("tangent", [0, 0.5, -1, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, math.inf),
+        ("miss", [0, 2, -1, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, math.inf),
+        ("behind", [0, 0, 1, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, math.inf),
+        ("inside -> far root, back face", [0, 0, 0, 1.0], [0, 0, 0.2], [0, 0, -1], 1e-3, math.inf),
+        ("tmin straddle: near root <= tmin", [0, 0, -1, 0.5], [0, 0, -0.5005], [0, 0, -1], 1e-3, math.inf),
+        ("t-max cut", [0, 0, -10, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, 5.0),
+        ("t-max between roots", [0, 0, -1, 0.5], [0, 0, 0], [0, 0, -1], 1e-3, 0.75),
+        ("ground r=100", [0, -100.5, -1, 100.0], [-2, 2, 1], [1.9, -2.4, -2.3], 1e-3, math.inf),
+        ("oblique", [1, 0, -1, 0.5], [-2, 2, 1], [3.1, -1.95, -1.8], 1e-3, math.inf),
+    ]
+    for name, s, o, d, tmin, tmax in cases:
+        r = sphere_hit(s, o, d, tmin, tmax)
+        k["sphere_hit"].append({"name": name, "sphere": s, "o": o, "d": d, "tmin": tmin,
+                                "tmax": "inf" if math.isinf(tmax) else tmax, "out": r})
+    for v, n in [([1, -1, 0], [0, 1, 0]), ([0.3, -0.4, 2.0], unit([0.2, 1, -0.1])), ([0, 0, -1], [0, 0, 1])]:
+        k["reflect"].append({"v": v, "n": n, "out": reflect(v, n)})
+    for uv, n, e in [(unit([1, -1, 0]), [0, 1, 0], 1 / 1.5), (unit([0.2, -1, 0.1]), [0, 1, 0], 1.5),
+                     ([0, -1, 0], [0, 1, 0], 1 / 1.5), (unit([1, -0.2, 0]), [0, 1, 0], 1.5)]:
+        k["refract"].append({"uv": uv, "n": n, "eta": e, "out": refract(uv, n, e)})
+    for c, ri in [(0.0, 1.5), (1.0, 1.5), (0.5, 1 / 1.5), (0.25, 1.5), (0.9, 1.0)]:
+        k["reflectance"].append({"cos": c, "ri": ri, "out": reflectance(c, ri)})
+    for c in [0.0, -1.0, 0.25, 0.5, 0.998, 0.999, 1.0, 2.0, 1e-9, 0.0625, 0.1, 0.9]:
+        k["quantize"].append({"c": c, "out": quantize(c)})
+    k["quantize"].append({"c": "nan", "out": 0})
+    cams = [("reference", 400, 225, 20.0, [-2, 2, 1], [0, 0, -1], [0, 1, 0], 10.0, 3.4),
+            ("cover C1", 1200, 675, 20.0, [13, 2, 3], [0, 0, 0], [0, 1, 0], 0.6, 10.0),
+            ("cover C0", 200, 112, 20.0, [13, 2, 3], [0, 0, 0], [0, 1, 0], 0.6, 10.0),
+            ("no defocus", 64, 36, 90.0, [0, 0, 0], [0, 0, -1], [0, 1, 0], 0.0, 1.0)]
+    for name, w, h, vfov, lf, la, up, da, fd in cams:
+        k["camera"].append({"name": name, "w": w, "h": h, "vfov": vfov, "look_from": lf, "look_at": la, "vup": up,
+                            "defocus_angle": da, "focus_dist": fd, "out": camera(w, h, vfov, lf, la, up, da, fd)})
+    for u, n in [([0.6, 0.0, 0.8], [0, 1, 0]), ([0, -1, 0], [0, 1, 0]), ([0, -1 + 5e-9, 0], [0, 1, 0])]:
+        k["lambertian_dir"].append({"unit": u, "n": n, "out": lambertian_dir(u, n)})
+    for d, n, fz, u in [([1, -1, 0], [0, 1, 0], 0.0, [0, 0, 1]), ([1, -1, 0], [0, 1, 0], 1.0, [0, -1, 0]),
+                        ([2, -0.5, 1], unit([0, 1, 0.3]), 0.3, unit([1, 1, 1])), ([1, -0.01, 0], [0, 1, 0], 0.5,
+                                                                                  [0, -1, 0])]:
+        ok, r = metal_dir(d, n, fz, u)
+        k["metal_dir"].append({"d": d, "n": n, "fuzz": fz, "unit": u, "scattered": ok, "out": r})
+    for d, n, fr, eta, xi in [([1, -1, 0], [0, 1, 0], True, 1.5, 0.99), ([1, -1, 0], [0, 1, 0], True, 1.5, 0.0),
+                              ([1, -0.2, 0], [0, 1, 0], False, 1.5, 0.5), ([0, -1, 0], [0, 1, 0], True, 1.5, 0.5),
+                              ([0.3, -1, 0.2], [0, 1, 0], False, 1 / 1.5, 0.9)]:
+        refl, r = dielectric_dir(d, n, fr, eta, xi)
+        k["dielectric_dir"].append({"d": d, "n": n, "front": fr, "eta": eta, "xi": xi, "reflected": refl, "out": r})
+    return k
+
+
+def main():
+    if REF_PPM.exists():
+        img = read_p3(REF_PPM)
+        np.savez_compressed(HERE / "scene_ppm.npz", pixels=img)
+        st = image_stats(img)
+        st["source"] = "reference scene.ppm (clojure -M:main output; spp 100, depth 50 per SURVEY.md §4)"
+        st["sha256"] = hashlib.sha256(REF_PPM.read_bytes()).hexdigest()
+        (HERE / "scene_ppm_stats.json").write_text(json.dumps(st, indent=1))
+        print("scene.ppm", img.shape, st["mean"])
+    else:
+        print("no /root/reference/scene.ppm here: keeping the committed scene fixtures")
+    (HERE / "kats.json").write_text(json.dumps(kats(), indent=1))
+    rng = [{"seed": s, "pixel": p, "sample": k, "draws": stream(s, p, k, 8)}
+           for s, p, k in [(1, 0, 0), (1, 0, 1), (1, 1, 0), (7, 12345, 99), (2**40 + 3, 810000 - 1, 1999)]]
+    (HERE / "rng_golden.json").write_text(json.dumps(rng, indent=1))
+    # small fp32-mirror renders (regression pins; oracle = test infrastructure)
+    sys.path[:0] = [str(ROOT), str(ROOT / "raytracing-clj_amd")]
+    import oracle
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = R.Scene.from_bodies(R.hittables)
+    cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
+    ref, _, segs_r, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+                                      sc.mat.astype(np.float64), cam.as_list(), cam.defocus, 48, 27, 8, 50, seed=3)
+    cs = scenes.cover(11)
+    cc = scenes.cover_camera(32, 18)
+    cov, _, segs_c, _ = oracle.render(oracle.MODE_MIRROR32, cs.sphere.astype(np.float64), cs.kind,
+                                      cs.mat.astype(np.float64), cc.as_list(), cc.defocus, 32, 18, 4, 50, seed=5)
+    np.savez_compressed(HERE / "mirror_small.npz", reference_48x27_spp8_seed3=ref, cover_32x18_spp4_seed5=cov,
+                        segments=np.array([segs_r, segs_c], np.int64))
+    print("kats, rng, mirror fixtures written")
+
+
+if __name__ == "__main__":
+    main()

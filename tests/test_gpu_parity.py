@@ -208,3 +208,45 @@ def test_bad_material_rejected(gpu_lib):
     with pytest.raises(RTError) as ei:
         R.render(sc, cam, 8, 8, spp=1)
     assert ei.value.code == -2
+
+
+def test_gpu_matches_committed_mirror_fixture(gpu_lib):
+    """Committed golden vectors (tests/golden/mirror_small.npz): bit-exact."""
+    from pathlib import Path
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    f = np.load(Path(__file__).parent / "golden" / "mirror_small.npz")
+    st = {}
+    g = R.render(_ref_scene(), R.camera(48, 27, **R.REFERENCE_CAMERA), 48, 27, spp=8, seed=3, stats=st)
+    assert np.array_equal(g, f["reference_48x27_spp8_seed3"]) and st["segments"] == f["segments"][0]
+    g = R.render(scenes.cover(11), scenes.cover_camera(32, 18), 32, 18, spp=4, seed=5, stats=st)
+    assert np.array_equal(g, f["cover_32x18_spp4_seed5"]) and st["segments"] == f["segments"][1]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_reproduces_reference_scene_ppm(gpu_lib, seed):
+    """Full reference config (400x225, 100 spp, depth 50) vs the reference's
+    own scene.ppm, within SURVEY.md §8c's statistical tolerance."""
+    from rtclj import raytracing as R
+    from test_oracle_pinning import within_tolerance
+    rgb = R.main(100, 50, out_path="/tmp/rtclj_scene_gpu.ppm", seed=seed)
+    ok, info = within_tolerance(rgb)
+    assert all(ok.values()), (ok, info)
+    assert np.array_equal(R.read_ppm("/tmp/rtclj_scene_gpu.ppm"), rgb)
+
+
+def test_c1_frame_properties(gpu_lib):
+    """BASELINE config C1 at full size (1200x675x100spp, cover scene): finite,
+    in-range, deterministic, and its top rows match the mirror bit for bit."""
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = scenes.cover(11)
+    cam = scenes.cover_camera(1200, 675)
+    st = {}
+    a = R.render(sc, cam, 1200, 675, spp=100, max_depth=50, seed=1, stats=st)
+    b = R.render(sc, cam, 1200, 675, spp=100, max_depth=50, seed=1)
+    assert np.array_equal(a, b)
+    assert np.isfinite(a).all() and a.min() >= 0 and a.max() <= 1.0 + 1e-6
+    assert 2.5 < st["segments"] / st["samples"] < 2.9
+    ref, _, _ = _mirror(sc, cam, 1200, 675, 100, 50, seed=1, rows=(300, 302))
+    _assert_parity(a[300:302], ref, "C1 rows 300-301")
