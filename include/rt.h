@@ -167,10 +167,29 @@ int rt_scene_free(rt_dscene* ds);
 int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
 
-/* Kernel variant selector for A/B measurement: 0 = default, 1 = sphere table
- * in LDS, 2 = sphere table through the scalar (constant) cache.  Returns the
- * previous value; applies to subsequent launches in this process. */
+/* Kernel variant selector for A/B measurement (all variants give identical
+ * bits): 0 = default (5); 1 = sphere table in LDS, one body per step;
+ * 2 = table through the scalar cache, one body per step; 4 = LDS table,
+ * bodies in groups of 4 with the next group prefetched; 5 = scalar-cache
+ * table, grouped; 3, 6, 7 = 1, 4, 5 with wave-level statistics counters
+ * (diagnostic builds; slower).  Returns the previous value; applies to
+ * subsequent launches in this process. */
 int rt_set_variant(int variant);
+
+/* Lanes per pixel (1, 2, 4; 0 = automatic by frame size): how many lanes
+ * share one pixel's four sample stripes.  Changes the launch shape, never the
+ * result.  Returns the previous value. */
+int rt_set_lanes_per_pixel(int lpp);
+
+/* Diagnostic counters of variant 3 since the last call (then cleared):
+ * [wave loop iterations, active lanes summed over them, body tests issued per
+ *  wave, candidate blocks entered per wave, lanes active in those blocks,
+ *  waves, 0, 0].  Synchronises the device. */
+int rt_debug_stats(uint64_t* out8);
+
+/* Diagnostic wave timeline of variant 3's last launches: n_waves x
+ * {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID}; returns the count. */
+int rt_debug_waves(uint64_t* out, size_t n_waves);
 
 int rt_device_count(void);
 const char* rt_last_error(void);

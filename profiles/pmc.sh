@@ -1,0 +1,26 @@
+#!/bin/bash
+# PMC recipe (MI355X_MICROARCH.md §rocprofv3 / §HBM): one counter group per
+# rocprofv3 pass, kernel-trace + stats only (no sys/runtime traces), on the
+# bench's own command.  Usage (on the GPU box, from the repo root):
+#   profiles/pmc.sh gpurun_out/pmc [extra bench.py args]
+# Writes <out>/<pass>/prof_counter_collection.csv per pass.
+set -u
+OUT=${1:?outdir}; shift
+REPO=$PWD
+cd /tmp && export TMPDIR=/tmp && cd "$REPO" || exit 1
+mkdir -p "$OUT"
+BENCH=(python3 bench.py --cpu-baseline off --steps 2 --warmup 1 "$@")
+pass() {
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o prof \
+    --pmc "$@" -- "${BENCH[@]}" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  case $rc in 124|134|137|139) echo "stopping: GPU step failed ($rc)"; exit $rc ;; esac
+  return 0
+}
+pass waves SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
+pass insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU
+pass lds SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE

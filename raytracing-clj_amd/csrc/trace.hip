@@ -47,9 +47,13 @@ struct alignas(16) KArgs {
   const int* kind;     // n: material kind
   float* out;          // rows_out x width x 3
   unsigned long long* counters;  // NULL or [segments, samples]
+  unsigned long long* dbg;       // stats build only: [wave iters, active lanes, sphere iters,
+                                 //  candidate blocks, lanes in blocks, waves]
+  unsigned long long* dbgw;      // stats build only: per wave {t_start, t_end, hw_id, xcc_id}
   float cam[18];       // center, p00, du, dv, disk_u, disk_v
   int defocus;
   int n;
+  int n_pad;           // geo entries: n rounded up to 4, plus 4 never-hit pads
   int width;
   int rows_out;
   int row_begin, row_tile, tile_first, tile_step;
@@ -91,22 +95,48 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
 
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1 };
 
-template <int SRC>
+// Sample stripes (arithmetic contract): a pixel's spp samples are split into
+// P = min(4, spp) contiguous stripes (stripe s: samples [s*q + min(s,r),
+// +q + (s<r)), q = spp/P, r = spp%P); each stripe is summed sequentially in
+// sample order, and the pixel total is ((s0 + s1) + s2) + s3, then / spp.
+// LPP lanes work on one pixel (1, 2 or 4; LPP > 1 needs P == 4): lane group
+// g runs stripes [g*4/LPP, (g+1)*4/LPP) back to back; the groups' stripe sums
+// are combined in stripe order after the loop (cross-lane), so every LPP
+// gives the same bits.  A wave covers 64/LPP pixels (8x8, 8x4 or 4x4).
+__device__ __forceinline__ int stripe_begin(int s, int spp, int P) {
+  const int q = spp / P, r = spp % P;
+  return s * q + (s < r ? s : r);
+}
+
+template <int SRC, int SCAN, int LPP, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
+  static_assert(LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel");
+  uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
+  uint64_t st_t0 = 0;
+  if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
   if constexpr (SRC == SRC_LDS) {
-    for (int i = threadIdx.x; i < n; i += 256) s_geo[i] = a.geo[i];
+    for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = a.geo[i];
     __syncthreads();
   }
 
-  // lane -> pixel: wave w of the block owns the 8x8 tile (w&1, w>>1).
+  // lane -> (pixel, stripe group): a wave owns a TW x TH pixel tile
+  // (PX = 64/LPP pixels), lane group grp = lane / PX; the block's 4 waves
+  // tile 2 x 2.
+  constexpr int PX = 64 / LPP;
+  constexpr int TW = (LPP == 4) ? 4 : 8;
+  constexpr int TH = (LPP == 1) ? 8 : 4;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int ro = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-  bool active = (px < a.width) && (ro < a.rows_out);
+  const int pl = lane % PX;     // pixel within the wave tile
+  const int grp = lane / PX;    // stripe group
+  const int px = blockIdx.x * (2 * TW) + (wave & 1) * TW + (pl % TW);
+  const int ro = blockIdx.y * (2 * TH) + (wave >> 1) * TH + (pl / TW);
+  const bool in_image = (px < a.width) && (ro < a.rows_out);
+  bool active = in_image;
 
   // compacted output row -> global image row (interleaved row tiles)
   int gy = a.row_begin + ro;
@@ -119,10 +149,18 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const uint32_t pkey = mix32(a.key ^ mix32(static_cast<uint32_t>(gy) * static_cast<uint32_t>(a.width) +
                                             static_cast<uint32_t>(px)));
 
-  float accr = 0.0f, accg = 0.0f, accb = 0.0f;
+  // this lane's samples [k, k_end) = stripes [grp*SPL, (grp+1)*SPL)
+  const int P = a.spp < 4 ? (a.spp > 0 ? a.spp : 1) : 4;
+  constexpr int SPL = 4 / LPP;  // stripes per lane (LPP > 1 requires P == 4)
+  int k = LPP == 1 ? 0 : stripe_begin(grp * SPL, a.spp, P);
+  const int k_end = LPP == 1 ? a.spp : stripe_begin(grp * SPL + SPL, a.spp, P);
+  int stripe = LPP == 1 ? 0 : grp * SPL;             // current stripe index
+  int k_next = stripe_begin(stripe + 1, a.spp, P);   // its end
+  float accr = 0.0f, accg = 0.0f, accb = 0.0f;       // current stripe sum
+  float totr = 0.0f, totg = 0.0f, totb = 0.0f;       // LPP == 1: running total
+  float s0r = 0.0f, s0g = 0.0f, s0b = 0.0f;          // LPP == 2: the lane's first stripe sum
   uint32_t segs = 0;
-  int k = 0;
-  if (a.spp <= 0 || a.max_depth <= 0) active = false;  // ray-color depth<=0 -> black (:46-47)
+  if (a.spp <= 0 || a.max_depth <= 0 || k >= k_end) active = false;  // depth<=0 -> black (:46-47)
 
   // path state
   uint32_t st = 0;
@@ -133,6 +171,13 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   bool fresh = true;
 
   while (active) {
+    if constexpr (STATS) {  // counted once per wave event, by its first active lane
+      const uint64_t ex = __builtin_amdgcn_read_exec();
+      if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+        ++st_iter;
+        st_lanes += __popcll(ex);
+      }
+    }
     if (fresh) {
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
       st = mix32(pkey + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
@@ -174,29 +219,80 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
     float best_t = INFINITY;
     int best = -1;
-#pragma unroll 4
-    for (int s = 0; s < n; ++s) {
-      float4 g;
-      if constexpr (SRC == SRC_LDS) g = s_geo[s];
-      else g = a.geo[s];
-      // hittable.clj:10-14 with a unit direction: a = 1, h = u.oc,
-      // c = |oc|^2 - r^2 (y first: the big ground sphere cancels exactly in the fma)
-      const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
-      const float h = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
-      const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
-      const float disc = fmaf(h, h, -c);
-      // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
-      if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) {
-        // the body the ray is leaving: exact arithmetic has c = 0 there
-        // (origin on its surface), so sq = |h| (self-hit acne guard)
-        const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
-        float t = h - sq;                 // nearer root (:15)
-        if (!(t > tmin)) t = h + sq;      // farther root (:16-18)
-        if (t > tmin && t < best_t) {     // open interval, strictly closer (:19, :35-42)
-          best_t = t;
-          best = s;
+    // the candidate block: roots, root choice, strict closest test.  The body
+    // the ray is leaving gets sq = |h| (exact arithmetic has c = 0 there:
+    // the origin lies on its surface) -- the self-hit acne guard.
+    auto consider = [&](float h, float disc, int s) {
+      if constexpr (STATS) {
+        const uint64_t ex = __builtin_amdgcn_read_exec();
+        if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+          ++st_blk;
+          st_blk_lanes += __popcll(ex);
         }
       }
+      const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
+      float t = h - sq;                 // nearer root (hittable.clj:15)
+      if (!(t > tmin)) t = h + sq;      // farther root (:16-18)
+      if (t > tmin && t < best_t) {     // open interval, strictly closer (:19, raytracing.clj:35-42)
+        best_t = t;
+        best = s;
+      }
+    };
+    if constexpr (SCAN == SCAN_SIMPLE) {
+#pragma unroll 4
+      for (int s = 0; s < n; ++s) {
+        float4 g;
+        if constexpr (SRC == SRC_LDS) g = s_geo[s];
+        else g = a.geo[s];
+        // hittable.clj:10-14 with a unit direction: a = 1, h = u.oc,
+        // c = |oc|^2 - r^2 (y first: the big ground sphere cancels exactly in the fma)
+        const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
+        const float h = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
+        const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
+        const float disc = fmaf(h, h, -c);
+        // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
+        if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) consider(h, disc, s);
+      }
+    } else {
+      // groups of 4 bodies; the next group is loaded before the current one is
+      // tested (hides the LDS / scalar-cache latency); one branch per group.
+      // The table is padded to a multiple of 4 (+4) with bodies that can never
+      // be candidates (-r^2 = +inf -> disc = -inf).
+      // Candidate test min(disc, max(h, -c)) >= 0 admits, beyond the simple
+      // form, only c == 0 & h < 0 (roots 2h and 0, rejected by t > tmin) and
+      // NaN disc (t NaN, rejected): identical results.
+      auto load = [&](int s) -> float4 {
+        if constexpr (SRC == SRC_LDS) return s_geo[s];
+        else return a.geo[s];
+      };
+      float4 g0 = load(0), g1 = load(1), g2 = load(2), g3 = load(3);
+      for (int s = 0; s < n; s += 4) {
+        const float4 n0 = load(s + 4), n1 = load(s + 5), n2 = load(s + 6), n3 = load(s + 7);
+        float h[4], disc[4];
+        bool cand[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 g = k == 0 ? g0 : k == 1 ? g1 : k == 2 ? g2 : g3;
+          const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
+          h[k] = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
+          const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
+          disc[k] = fmaf(h[k], h[k], -c);
+          cand[k] = fminf(disc[k], fmaxf(h[k], -c)) >= 0.0f;
+        }
+        if (cand[0] | cand[1] | cand[2] | cand[3]) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (cand[k]) consider(h[k], disc[k], s + k);
+        }
+        g0 = n0;
+        g1 = n1;
+        g2 = n2;
+        g3 = n3;
+      }
+    }
+    if constexpr (STATS) {
+      const uint64_t ex = __builtin_amdgcn_read_exec();
+      if (lane == __ffsll(static_cast<long long>(ex)) - 1) st_sph += static_cast<uint64_t>(n);
     }
 
     bool done = false;
@@ -303,23 +399,83 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       accg += cg;
       accb += cb;
       fresh = true;
-      if (++k >= a.spp) active = false;
+      if (++k == k_next || k >= k_end) {
+        // a stripe is complete (the contract's sequential stripe sum)
+        if constexpr (LPP == 1) {
+          totr += accr;
+          totg += accg;
+          totb += accb;
+          accr = accg = accb = 0.0f;
+        } else if constexpr (LPP == 2) {
+          if (stripe == grp * SPL) {
+            s0r = accr;
+            s0g = accg;
+            s0b = accb;
+            accr = accg = accb = 0.0f;
+          }
+        }
+        ++stripe;
+        k_next = stripe_begin(stripe + 1, a.spp, P);
+      }
+      if (k >= k_end) active = false;
     }
   }
 
-  if (px < a.width && ro < a.rows_out) {
+  // ---- per-pixel total ((s0 + s1) + s2) + s3, / spp (raytracing.clj:155) ----
+  float outr, outg, outb;
+  if constexpr (LPP == 1) {
+    outr = totr;
+    outg = totg;
+    outb = totb;
+  } else if constexpr (LPP == 2) {
+    // group 0 holds s0 (s0*) and s1 (acc*); group 1 holds s2 (s0*) and s3 (acc*)
+    const float s2r = __shfl(s0r, pl + PX), s2g = __shfl(s0g, pl + PX), s2b = __shfl(s0b, pl + PX);
+    const float s3r = __shfl(accr, pl + PX), s3g = __shfl(accg, pl + PX), s3b = __shfl(accb, pl + PX);
+    outr = ((s0r + accr) + s2r) + s3r;
+    outg = ((s0g + accg) + s2g) + s3g;
+    outb = ((s0b + accb) + s2b) + s3b;
+  } else {
+    // group g holds stripe g in acc*
+    const float s1r = __shfl(accr, pl + PX), s1g = __shfl(accg, pl + PX), s1b = __shfl(accb, pl + PX);
+    const float s2r = __shfl(accr, pl + 2 * PX), s2g = __shfl(accg, pl + 2 * PX), s2b = __shfl(accb, pl + 2 * PX);
+    const float s3r = __shfl(accr, pl + 3 * PX), s3g = __shfl(accg, pl + 3 * PX), s3b = __shfl(accb, pl + 3 * PX);
+    outr = ((accr + s1r) + s2r) + s3r;
+    outg = ((accg + s1g) + s2g) + s3g;
+    outb = ((accb + s1b) + s2b) + s3b;
+  }
+  if (in_image && grp == 0) {
     const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
     float* o = a.out + (static_cast<size_t>(ro) * a.width + px) * 3;
-    o[0] = accr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
-    o[1] = accg / inv;
-    o[2] = accb / inv;
+    o[0] = outr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
+    o[1] = outg / inv;
+    o[2] = outb / inv;
   }
 
+  if constexpr (STATS) {
+    if (a.dbg && st_iter) {
+      atomicAdd(&a.dbg[0], static_cast<unsigned long long>(st_iter));
+      atomicAdd(&a.dbg[1], static_cast<unsigned long long>(st_lanes));
+      atomicAdd(&a.dbg[2], static_cast<unsigned long long>(st_sph));
+    }
+    if (a.dbg && st_blk) {
+      atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
+      atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
+    }
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+    if (a.dbgw && lane == 0) {
+      const size_t wid = (static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+      if (wid < 65536) {
+        a.dbgw[4 * wid + 0] = st_t0;
+        a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        a.dbgw[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        a.dbgw[4 * wid + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+      }
+    }
+  }
   if (a.counters) {
     // one 64-bit atomic per wave: segments and samples of its 64 lanes
     uint32_t v = segs;
-    uint32_t smp = (px < a.width && ro < a.rows_out && a.max_depth > 0 && a.spp > 0)
-                       ? static_cast<uint32_t>(a.spp) : 0u;
+    uint32_t smp = (in_image && grp == 0 && a.max_depth > 0 && a.spp > 0) ? static_cast<uint32_t>(a.spp) : 0u;
     for (int off = 32; off > 0; off >>= 1) {
       v += __shfl_xor(v, off);
       smp += __shfl_xor(smp, off);
@@ -332,7 +488,55 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 }
 
 // ------------------------------------------------------------- host ------
-static int g_variant = 0;  // 0 default (= LDS), 1 LDS, 2 scalar
+// Kernel variants (rt_set_variant):
+//   1 LDS table, simple scan        2 scalar-cache table, simple scan
+//   3 = 1 + stats                   4 LDS table, grouped scan (prefetch)
+//   5 scalar, grouped scan          6 = 4 + stats        7 = 5 + stats
+//   0 = default (5)
+// Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
+// 0 = automatic (enough waves to keep the chip full to the end).
+struct Variant {
+  const void* fn[3];   // LPP 1, 2, 4
+  bool lds;
+  bool stats;
+};
+#define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
+static const Variant& variant_table(int v) {
+  static const Variant t[8] = {
+      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, false), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, false),
+        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, false)}, false, false},
+      {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
+      {{RT_K(SRC_SCALAR, SCAN_SIMPLE, 1, false), nullptr, nullptr}, false, false},
+      {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, true), nullptr, nullptr}, true, true},
+      {{RT_K(SRC_LDS, SCAN_GROUP4, 1, false), RT_K(SRC_LDS, SCAN_GROUP4, 2, false),
+        RT_K(SRC_LDS, SCAN_GROUP4, 4, false)}, true, false},
+      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, false), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, false),
+        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, false)}, false, false},
+      {{RT_K(SRC_LDS, SCAN_GROUP4, 1, true), RT_K(SRC_LDS, SCAN_GROUP4, 2, true),
+        RT_K(SRC_LDS, SCAN_GROUP4, 4, true)}, true, true},
+      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, true), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, true),
+        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, true)}, false, true},
+  };
+  return t[(v >= 0 && v < 8) ? v : 0];
+}
+#undef RT_K
+static int g_lpp = 0;  // 0 = automatic
+
+// Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
+// last waves then drain quickly); 1 lane keeps the SIMD fuller per wave.
+static int choose_lpp(int width, int rows, int spp, bool have_all) {
+  if (!have_all || spp < 4) return 1;
+  if (g_lpp == 1 || g_lpp == 2 || g_lpp == 4) return g_lpp;
+  const long long target = 48 * 1024;  // ~6 x the waves an MI355X keeps resident
+  const long long w1 = 4LL * ((width + 15) / 16) * ((rows + 15) / 16);
+  const long long w2 = 4LL * ((width + 15) / 16) * ((rows + 7) / 8);
+  if (w1 >= target) return 1;
+  if (w2 >= target) return 2;
+  return 4;
+}
+static int g_variant = 0;
+static unsigned long long* g_dbg = nullptr;   // device u64[8] for variant 3 (per process, device 0)
+static unsigned long long* g_dbgw = nullptr;  // device u64[4 * 65536] wave timeline for variant 3
 
 }  // namespace rtclj
 
@@ -341,6 +545,7 @@ using namespace rtclj;
 struct rt_dscene {
   int device;
   int n;
+  int n_pad;
   float4* geo;
   float4* sph;
   float4* mat;
@@ -359,7 +564,13 @@ static int hip_fail(hipError_t e, const char* what) {
 
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
-  if (v >= 0 && v <= 2) g_variant = v;
+  if (v >= 0 && v <= 7) g_variant = v;
+  return old;
+}
+
+extern "C" int rt_set_lanes_per_pixel(int lpp) {
+  const int old = g_lpp;
+  if (lpp == 0 || lpp == 1 || lpp == 2 || lpp == 4) g_lpp = lpp;
   return old;
 }
 
@@ -386,8 +597,10 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
                                      " not available (" + std::to_string(ndev) + " visible)");
   HIP_TRY(hipSetDevice(device));
   const int n = s->n;
+  const int n_pad = ((n + 3) / 4) * 4 + 4;   // grouped scan reads up to 4 past the last group
   const size_t cnt = n > 0 ? n : 1;
-  std::vector<float4> geo(cnt), sph(cnt), mat(cnt);
+  // pads: -r^2 = +inf -> c = +inf, disc = -inf: never a candidate
+  std::vector<float4> geo(n_pad, make_float4(0.0f, 0.0f, 0.0f, INFINITY)), sph(cnt), mat(cnt);
   std::vector<int> kind(cnt, 0);
   for (int i = 0; i < n; ++i) {
     const float* q = s->sphere + 4 * i;
@@ -398,12 +611,12 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     mat[i] = make_float4(m[0], m[1], m[2], m[3]);
     kind[i] = s->mat_kind[i];
   }
-  rt_dscene* d = new rt_dscene{device, n, nullptr, nullptr, nullptr, nullptr};
-  hipError_t e = hipMalloc(&d->geo, cnt * sizeof(float4));
+  rt_dscene* d = new rt_dscene{device, n, n_pad, nullptr, nullptr, nullptr, nullptr};
+  hipError_t e = hipMalloc(&d->geo, n_pad * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&d->sph, cnt * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&d->mat, cnt * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&d->kind, cnt * sizeof(int));
-  if (e == hipSuccess) e = hipMemcpy(d->geo, geo.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d->geo, geo.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d->sph, sph.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d->mat, mat.data(), cnt * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d->kind, kind.data(), cnt * sizeof(int), hipMemcpyHostToDevice);
@@ -449,6 +662,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   std::memcpy(a.cam + 15, c->disk_v, 12);
   a.defocus = c->defocus ? 1 : 0;
   a.n = ds->n;
+  a.n_pad = ds->n_pad;
   a.width = p->width;
   a.rows_out = rows;
   a.row_begin = p->row_begin;
@@ -461,22 +675,56 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
-  const dim3 grid((p->width + 15) / 16, (rows + 15) / 16);
+  const Variant& v = variant_table(g_variant);
+  const int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr);
+  const int tw = lpp == 4 ? 4 : 8, th = lpp == 1 ? 8 : 4;   // wave tile (trace_kernel)
+  const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
   const dim3 block(256);
+  const void* fn = v.fn[lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  if (g_variant == 2) {
-    hipLaunchKernelGGL(trace_kernel<SRC_SCALAR>, grid, block, 0, stream, a);
-  } else {
-    const size_t lds = static_cast<size_t>(ds->n > 0 ? ds->n : 1) * sizeof(float4);
-    static bool attr_set[64] = {};
-    if (ds->device < 64 && !attr_set[ds->device]) {
-      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<SRC_LDS>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  RT_MAX_SPHERES * static_cast<int>(sizeof(float4))));
-      attr_set[ds->device] = true;
+  if (v.stats) {
+    if (!g_dbg) {
+      HIP_TRY(hipMalloc(&g_dbg, 8 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(g_dbg, 0, 8 * sizeof(unsigned long long)));
+      HIP_TRY(hipMalloc(&g_dbgw, 4 * 65536 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(g_dbgw, 0, 4 * 65536 * sizeof(unsigned long long)));
     }
-    hipLaunchKernelGGL(trace_kernel<SRC_LDS>, grid, block, lds, stream, a);
+    a.dbg = g_dbg;
+    a.dbgw = g_dbgw;
   }
+  size_t lds = 0;
+  if (v.lds) {
+    lds = static_cast<size_t>(ds->n_pad) * sizeof(float4);
+    if (lds > 64 * 1024)
+      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  }
+  void* args[] = {&a};
+  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
   HIP_TRY(hipGetLastError());
   return RT_OK;
+}
+
+// Stats build (variant 3) read-back: copies and clears the 8 debug counters.
+extern "C" int rt_debug_stats(uint64_t* out8) {
+  if (!out8) return set_error(RT_E_ARG, "rt_debug_stats: NULL");
+  if (!g_dbg) {
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    return RT_OK;
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out8, g_dbg, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(g_dbg, 0, 8 * sizeof(uint64_t)));
+  return RT_OK;
+}
+
+// Stats build (variant 3) wave timeline: up to n waves x {t_start, t_end,
+// hw_id, xcc_id} (s_memrealtime ticks, 100 MHz); cleared after the copy.
+extern "C" int rt_debug_waves(uint64_t* out, size_t n_waves) {
+  if (!out) return set_error(RT_E_ARG, "rt_debug_waves: NULL");
+  if (!g_dbgw) return 0;
+  if (n_waves > 65536) n_waves = 65536;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, g_dbgw, 4 * n_waves * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(g_dbgw, 0, 4 * 65536 * sizeof(uint64_t)));
+  return static_cast<int>(n_waves);
 }

@@ -161,19 +161,47 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-def test_scalar_variant_matches_lds_variant(gpu_lib):
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("lpp", [1, 2, 4])
+def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
+    """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
+    stats builds) and lanes-per-pixel launch shapes all give the mirror's bits."""
     from rtclj import scenes
     from rtclj import raytracing as R
     from rtclj._lib import lib
     sc = scenes.cover(11)
-    cam = scenes.cover_camera(96, 54)
-    a = R.render(sc, cam, 96, 54, spp=4, seed=4)
-    old = lib.rt_set_variant(2)
+    w, h, spp = 72, 40, 7          # odd spp: unequal stripes (2,2,2,1)
+    cam = scenes.cover_camera(w, h)
+    ov, ol = lib.rt_set_variant(variant), lib.rt_set_lanes_per_pixel(lpp)
     try:
-        b = R.render(sc, cam, 96, 54, spp=4, seed=4)
+        st = {}
+        g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
+        if variant in (3, 6, 7):
+            import ctypes as C
+            d = (C.c_uint64 * 8)()
+            lib.rt_debug_stats(d)
     finally:
-        lib.rt_set_variant(old)
-    assert np.array_equal(a, b)
+        lib.rt_set_variant(ov)
+        lib.rt_set_lanes_per_pixel(ol)
+    ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4)
+    assert np.array_equal(g, ref), f"variant {variant} lpp {lpp}"
+    assert st["segments"] == segs
+
+
+@pytest.mark.parametrize("spp", [1, 2, 3, 4, 5, 100])
+def test_sample_stripes_edge_spp(gpu_lib, spp):
+    from rtclj import raytracing as R
+    from rtclj._lib import lib
+    sc = _ref_scene()
+    cam = R.camera(40, 22, **R.REFERENCE_CAMERA)
+    ref, _, _ = _mirror(sc, cam, 40, 22, spp, 20, seed=8)
+    for lpp in (0, 1, 2, 4):
+        old = lib.rt_set_lanes_per_pixel(lpp)
+        try:
+            g = R.render(sc, cam, 40, 22, spp=spp, max_depth=20, seed=8)
+        finally:
+            lib.rt_set_lanes_per_pixel(old)
+        assert np.array_equal(g, ref), (spp, lpp)
 
 
 def test_max_spheres_and_too_many(gpu_lib):
