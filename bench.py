@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp (not a bench line)")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant)")
+    ap.add_argument("--lpp", type=int, default=0, help="lanes per pixel (rt_set_lanes_per_pixel; 0 auto)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -116,6 +117,7 @@ def main():
     if world > 1:
         dist.init_process_group(backend=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
     lib.rt_set_variant(a.variant)
+    lib.rt_set_lanes_per_pixel(a.lpp)
 
     wl = dict(WORKLOADS[a.workload])
     if a.spp:

@@ -171,7 +171,8 @@ int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
  * bits): 0 = default (5); 1 = sphere table in LDS, one body per step;
  * 2 = table through the scalar cache, one body per step; 4 = LDS table,
  * bodies in groups of 4 with the next group prefetched; 5 = scalar-cache
- * table, grouped; 3, 6, 7 = 1, 4, 5 with wave-level statistics counters
+ * table, grouped; 8 / 9 = 4 / 5 with two bodies per packed-fp32
+ * instruction; 3, 6, 7, 10 = 1, 4, 5, 9 with wave-level statistics counters
  * (diagnostic builds; slower).  Returns the previous value; applies to
  * subsequent launches in this process. */
 int rt_set_variant(int variant);

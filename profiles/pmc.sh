@@ -19,8 +19,14 @@ pass() {
   case $rc in 124|134|137|139) echo "stopping: GPU step failed ($rc)"; exit $rc ;; esac
   return 0
 }
-pass waves SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
-pass insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU
-pass lds SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
+PASSES=${PMC_PASSES:-"waves insts lds sched fetch write"}
+for g in $PASSES; do
+  case $g in
+    waves) pass waves SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE ;;
+    insts) pass insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU ;;
+    lds)   pass lds SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH ;;
+    sched) pass sched SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_IFETCH SQ_LEVEL_WAVES SQ_ACCUM_PREV_HIRES ;;
+    fetch) pass fetch FETCH_SIZE ;;
+    write) pass write WRITE_SIZE ;;
+  esac
+done

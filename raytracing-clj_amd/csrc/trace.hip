@@ -41,7 +41,8 @@
 namespace rtclj {
 
 struct alignas(16) KArgs {
-  const float4* geo;   // n: cx, cy, cz, -r*r   (hit test)
+  const float4* geo;   // n_pad: cx, cy, cz, -r*r   (hit test)
+  const struct Pair* geo2;  // n_pad/2: the same, two bodies interleaved per Pair
   const float4* sph;   // n: cx, cy, cz, r      (hit record)
   const float4* mat;   // n: albedo rgb, fuzz | refraction index
   const int* kind;     // n: material kind
@@ -95,7 +96,14 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
 
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
-enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2 };
+
+// two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct alignas(16) Pair {
+  f2 x, y, z, w;   // centres and -r^2 of bodies 2p and 2p+1
+};
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Sample stripes (arithmetic contract): a pixel's spp samples are split into
 // P = min(4, spp) contiguous stripes (stripe s: samples [s*q + min(s,r),
@@ -119,7 +127,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
   if constexpr (SRC == SRC_LDS) {
-    for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = a.geo[i];
+    const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
+    for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
     __syncthreads();
   }
 
@@ -252,6 +261,41 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const float disc = fmaf(h, h, -c);
         // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
         if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) consider(h, disc, s);
+      }
+    } else if constexpr (SCAN == SCAN_PK4) {
+      // As SCAN_GROUP4, but the arithmetic of two bodies runs in one packed
+      // instruction (v_pk_add/mul/fma_f32: each half is the same IEEE-rounded
+      // op as the scalar form, so the bits are unchanged); the group's
+      // "any candidate" test is one max-reduction and one compare.
+      const Pair* tab;
+      if constexpr (SRC == SRC_LDS) tab = reinterpret_cast<const Pair*>(s_geo);
+      else tab = a.geo2;
+      const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
+      const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
+      Pair A = tab[0], B = tab[1];
+      for (int s = 0; s < n; s += 4) {
+        const Pair nA = tab[(s >> 1) + 2], nB = tab[(s >> 1) + 3];
+        f2 h[2], c[2], disc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const Pair& g = j == 0 ? A : B;
+          const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
+          h[j] = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
+          c[j] = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
+          disc[j] = fma2(h[j], h[j], -c[j]);
+        }
+        const float q0 = fminf(disc[0].x, fmaxf(h[0].x, -c[0].x));
+        const float q1 = fminf(disc[0].y, fmaxf(h[0].y, -c[0].y));
+        const float q2 = fminf(disc[1].x, fmaxf(h[1].x, -c[1].x));
+        const float q3 = fminf(disc[1].y, fmaxf(h[1].y, -c[1].y));
+        if (fmaxf(fmaxf(q0, q1), fmaxf(q2, q3)) >= 0.0f) {
+          if (q0 >= 0.0f) consider(h[0].x, disc[0].x, s);
+          if (q1 >= 0.0f) consider(h[0].y, disc[0].y, s + 1);
+          if (q2 >= 0.0f) consider(h[1].x, disc[1].x, s + 2);
+          if (q3 >= 0.0f) consider(h[1].y, disc[1].y, s + 3);
+        }
+        A = nA;
+        B = nB;
       }
     } else {
       // groups of 4 bodies; the next group is loaded before the current one is
@@ -492,6 +536,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 //   1 LDS table, simple scan        2 scalar-cache table, simple scan
 //   3 = 1 + stats                   4 LDS table, grouped scan (prefetch)
 //   5 scalar, grouped scan          6 = 4 + stats        7 = 5 + stats
+//   8 LDS table, packed pairs      9 scalar, packed pairs   10 = 9 + stats
 //   0 = default (5)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
 // 0 = automatic (enough waves to keep the chip full to the end).
@@ -502,7 +547,7 @@ struct Variant {
 };
 #define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
 static const Variant& variant_table(int v) {
-  static const Variant t[8] = {
+  static const Variant t[11] = {
       {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, false), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, false),
         RT_K(SRC_SCALAR, SCAN_GROUP4, 4, false)}, false, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
@@ -516,8 +561,14 @@ static const Variant& variant_table(int v) {
         RT_K(SRC_LDS, SCAN_GROUP4, 4, true)}, true, true},
       {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, true), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, true),
         RT_K(SRC_SCALAR, SCAN_GROUP4, 4, true)}, false, true},
+      {{RT_K(SRC_LDS, SCAN_PK4, 1, false), RT_K(SRC_LDS, SCAN_PK4, 2, false),
+        RT_K(SRC_LDS, SCAN_PK4, 4, false)}, true, false},
+      {{RT_K(SRC_SCALAR, SCAN_PK4, 1, false), RT_K(SRC_SCALAR, SCAN_PK4, 2, false),
+        RT_K(SRC_SCALAR, SCAN_PK4, 4, false)}, false, false},
+      {{RT_K(SRC_SCALAR, SCAN_PK4, 1, true), RT_K(SRC_SCALAR, SCAN_PK4, 2, true),
+        RT_K(SRC_SCALAR, SCAN_PK4, 4, true)}, false, true},
   };
-  return t[(v >= 0 && v < 8) ? v : 0];
+  return t[(v >= 0 && v < 11) ? v : 0];
 }
 #undef RT_K
 static int g_lpp = 0;  // 0 = automatic
@@ -547,6 +598,7 @@ struct rt_dscene {
   int n;
   int n_pad;
   float4* geo;
+  float4* geo2;   // n_pad/2 Pairs (= n_pad float4)
   float4* sph;
   float4* mat;
   int* kind;
@@ -564,7 +616,7 @@ static int hip_fail(hipError_t e, const char* what) {
 
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
-  if (v >= 0 && v <= 7) g_variant = v;
+  if (v >= 0 && v <= 10) g_variant = v;
   return old;
 }
 
@@ -611,8 +663,18 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     mat[i] = make_float4(m[0], m[1], m[2], m[3]);
     kind[i] = s->mat_kind[i];
   }
-  rt_dscene* d = new rt_dscene{device, n, n_pad, nullptr, nullptr, nullptr, nullptr};
+  // pair-interleaved copy for the packed scan: (x0 x1 y0 y1 z0 z1 w0 w1) per pair
+  std::vector<float> geo2(4 * static_cast<size_t>(n_pad));
+  for (int q = 0; q < n_pad / 2; ++q) {
+    const float4 b0 = geo[2 * q], b1 = geo[2 * q + 1];
+    float* o = &geo2[8 * static_cast<size_t>(q)];
+    o[0] = b0.x; o[1] = b1.x; o[2] = b0.y; o[3] = b1.y;
+    o[4] = b0.z; o[5] = b1.z; o[6] = b0.w; o[7] = b1.w;
+  }
+  rt_dscene* d = new rt_dscene{device, n, n_pad, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipError_t e = hipMalloc(&d->geo, n_pad * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&d->geo2, n_pad * sizeof(float4));
+  if (e == hipSuccess) e = hipMemcpy(d->geo2, geo2.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&d->sph, cnt * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&d->mat, cnt * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&d->kind, cnt * sizeof(int));
@@ -632,6 +694,7 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   if (!d) return RT_OK;
   (void)hipSetDevice(d->device);
   if (d->geo) (void)hipFree(d->geo);
+  if (d->geo2) (void)hipFree(d->geo2);
   if (d->sph) (void)hipFree(d->sph);
   if (d->mat) (void)hipFree(d->mat);
   if (d->kind) (void)hipFree(d->kind);
@@ -649,6 +712,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
   KArgs a{};
   a.geo = ds->geo;
+  a.geo2 = reinterpret_cast<const Pair*>(ds->geo2);
   a.sph = ds->sph;
   a.mat = ds->mat;
   a.kind = ds->kind;

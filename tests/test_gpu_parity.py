@@ -161,7 +161,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("lpp", [1, 2, 4])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
@@ -176,7 +176,7 @@ def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     try:
         st = {}
         g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7):
+        if variant in (3, 6, 7, 10):
             import ctypes as C
             d = (C.c_uint64 * 8)()
             lib.rt_debug_stats(d)

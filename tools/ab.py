@@ -58,7 +58,7 @@ def main():
             elif not np.array_equal(img, ref):
                 print(f"variant {name}: frame differs from variant {names[0]}!", flush=True)
                 sys.exit(1)
-            if v in (3, 6, 7):
+            if v in (3, 6, 7, 10):
                 d = (C.c_uint64 * 8)()
                 check(lib.rt_debug_stats(d))
                 d = list(d)
