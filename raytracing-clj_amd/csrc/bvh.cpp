@@ -1,0 +1,206 @@
+// bvh.cpp — host-side bounding-volume hierarchy over the scene's bodies, for
+// the kernel's BVH traversal variant (trace.hip, SCAN_BVH).
+//
+// It replaces nothing in the reference: the reference's hit-anything
+// (src/raytracing.clj:33-43) is a linear scan, and the traversal is built so
+// that the hit it returns is the scan's, bit for bit:
+//   * every body keeps its original index; the traversal accepts a closer t,
+//     or an equal t of a lower index (the scan's strict `t < closest` in
+//     array order picks the lowest index among equal t);
+//   * the body test itself is the scan's fp32 op sequence;
+//   * boxes are culled only conservatively (per-ray padding, trace.hip).
+// "Big" bodies (radius > 16 x the median, e.g. the r = 1000 ground) would
+// make every box huge; they are kept out of the tree and scanned first.
+//
+// Layout (device, all 16-byte aligned):
+//   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
+//                    slab tests, child refs: >= 0 node, < 0 leaf ~pair, INT_MIN empty
+//   pairs[n_pairs]   two bodies per leaf: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
+//                    a missing second body has w = +inf: never a candidate)
+//   pidx[n_pairs]    original indices of the two bodies (-1 for the pad)
+#include "bvh.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <numeric>
+
+namespace rtclj {
+
+namespace {
+
+struct Box {
+  float lo[3] = {INFINITY, INFINITY, INFINITY};
+  float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void add(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+};
+
+// exact float box of a body, rounded outward
+Box body_box(const float* s) {
+  Box b;
+  const float r = std::fabs(s[3]);
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = std::nextafter(s[k] - r, -INFINITY);
+    b.hi[k] = std::nextafter(s[k] + r, INFINITY);
+  }
+  return b;
+}
+
+struct Builder {
+  const float* sph;
+  std::vector<int> prim;   // original indices, permuted during the build
+  BvhHost* out;
+  int max_depth = 0;
+
+  int leaf(int lo, int cnt, Box* box) {
+    const int p = static_cast<int>(out->pidx.size() / 2);
+    float pair[8] = {0, 0, 0, 0, 0, 0, INFINITY, INFINITY};
+    int idx[2] = {-1, -1};
+    for (int j = 0; j < cnt; ++j) {
+      const float* s = sph + 4 * prim[lo + j];
+      pair[0 + j] = s[0];
+      pair[2 + j] = s[1];
+      pair[4 + j] = s[2];
+      pair[6 + j] = -(s[3] * s[3]);
+      idx[j] = prim[lo + j];
+      box->add(body_box(s));
+    }
+    out->pairs.insert(out->pairs.end(), pair, pair + 8);
+    out->pidx.push_back(idx[0]);
+    out->pidx.push_back(idx[1]);
+    return ~p;   // < 0: leaf
+  }
+
+  // returns a child ref (node index >= 0, or ~leaf) and its box
+  int build(int lo, int hi, int depth, Box* box) {
+    max_depth = std::max(max_depth, depth);
+    const int cnt = hi - lo;
+    if (cnt <= 2) return leaf(lo, cnt, box);
+    Box cb;  // centroid bounds
+    for (int i = lo; i < hi; ++i) {
+      const float* s = sph + 4 * prim[i];
+      for (int k = 0; k < 3; ++k) {
+        cb.lo[k] = std::min(cb.lo[k], s[k]);
+        cb.hi[k] = std::max(cb.hi[k], s[k]);
+      }
+    }
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    // median split on an even boundary: balanced depth, full leaf pairs
+    int mid = lo + ((cnt / 2 + 1) & ~1);
+    if (mid >= hi) mid = lo + 2;
+    std::nth_element(prim.begin() + lo, prim.begin() + mid, prim.begin() + hi, [&](int a, int b) {
+      const float ca = sph[4 * a + axis], cb_ = sph[4 * b + axis];
+      return ca < cb_ || (ca == cb_ && a < b);
+    });
+    const int me = static_cast<int>(out->nodes.size());
+    out->nodes.emplace_back();
+    Box b0, b1;
+    const int c0 = build(lo, mid, depth + 1, &b0);
+    const int c1 = build(mid, hi, depth + 1, &b1);
+    BvhNode& n = out->nodes[me];
+    const Box* bx[2] = {&b0, &b1};
+    for (int c = 0; c < 2; ++c) {
+      n.minx[c] = bx[c]->lo[0];
+      n.miny[c] = bx[c]->lo[1];
+      n.minz[c] = bx[c]->lo[2];
+      n.maxx[c] = bx[c]->hi[0];
+      n.maxy[c] = bx[c]->hi[1];
+      n.maxz[c] = bx[c]->hi[2];
+    }
+    n.child[0] = c0;
+    n.child[1] = c1;
+    box->add(b0);
+    box->add(b1);
+    return me;
+  }
+};
+
+}  // namespace
+
+int bvh_build(const float* sph, int n, BvhHost* out) {
+  *out = BvhHost{};
+  // big bodies: scanned first, outside the tree
+  std::vector<float> radii;
+  for (int i = 0; i < n; ++i) radii.push_back(std::fabs(sph[4 * i + 3]));
+  float med = 0.0f;
+  if (n > 0) {
+    std::vector<float> tmp = radii;
+    std::nth_element(tmp.begin(), tmp.begin() + n / 2, tmp.end());
+    med = tmp[n / 2];
+  }
+  Builder b{sph, {}, out};
+  for (int i = 0; i < n; ++i) {
+    const bool finite = std::isfinite(sph[4 * i]) && std::isfinite(sph[4 * i + 1]) &&
+                        std::isfinite(sph[4 * i + 2]) && std::isfinite(sph[4 * i + 3]);
+    if (!finite || (n > 8 && radii[i] > 16.0f * med && out->big.size() < 64))
+      out->big.push_back(i);
+    else
+      b.prim.push_back(i);
+  }
+  // bounding sphere of the tree's bodies (centre of their box, radius to the
+  // farthest surface): D = |O - centre| + radius bounds |oc| + r per ray
+  Box all;
+  for (int i : b.prim) all.add(body_box(sph + 4 * i));
+  double bc[3] = {0, 0, 0}, br = 0;
+  if (!b.prim.empty()) {
+    for (int k = 0; k < 3; ++k) bc[k] = 0.5 * (double(all.lo[k]) + all.hi[k]);
+    for (int i : b.prim) {
+      const float* s = sph + 4 * i;
+      const double dx = s[0] - bc[0], dy = s[1] - bc[1], dz = s[2] - bc[2];
+      br = std::max(br, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs(s[3]));
+    }
+  }
+  for (int k = 0; k < 3; ++k) out->center[k] = static_cast<float>(bc[k]);
+  out->radius = static_cast<float>(br * (1.0 + 1e-6)) + 1e-6f;
+  // root is always node 0 with two children (a leaf-only tree gets a root)
+  out->nodes.emplace_back();
+  const int cnt = static_cast<int>(b.prim.size());
+  Box b0, b1;
+  int c0 = INT_MIN, c1 = INT_MIN;
+  if (cnt > 0) {
+    const int mid = cnt <= 2 ? cnt : ((cnt / 2 + 1) & ~1);
+    // split the root by the same rule as build() (axis from centroid bounds)
+    if (cnt <= 2) {
+      c0 = b.leaf(0, cnt, &b0);
+    } else {
+      Box cb;
+      for (int i : b.prim)
+        for (int k = 0; k < 3; ++k) {
+          cb.lo[k] = std::min(cb.lo[k], sph[4 * i + k]);
+          cb.hi[k] = std::max(cb.hi[k], sph[4 * i + k]);
+        }
+      int axis = 0;
+      for (int k = 1; k < 3; ++k)
+        if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+      std::nth_element(b.prim.begin(), b.prim.begin() + mid, b.prim.end(), [&](int x, int y) {
+        const float cx = sph[4 * x + axis], cy = sph[4 * y + axis];
+        return cx < cy || (cx == cy && x < y);
+      });
+      c0 = b.build(0, mid, 1, &b0);
+      c1 = b.build(mid, cnt, 1, &b1);
+    }
+  }
+  BvhNode& root = out->nodes[0];
+  const Box* bx[2] = {&b0, &b1};
+  for (int c = 0; c < 2; ++c) {
+    root.minx[c] = bx[c]->lo[0];
+    root.miny[c] = bx[c]->lo[1];
+    root.minz[c] = bx[c]->lo[2];
+    root.maxx[c] = bx[c]->hi[0];
+    root.maxy[c] = bx[c]->hi[1];
+    root.maxz[c] = bx[c]->hi[2];
+  }
+  root.child[0] = c0;
+  root.child[1] = c1;
+  out->depth = b.max_depth + 1;
+  return 0;
+}
+
+}  // namespace rtclj

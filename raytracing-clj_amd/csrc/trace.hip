@@ -30,12 +30,14 @@
 // default), and no transcendental function is used.  See DESIGN.md §3.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "bvh.h"
 #include "rt_internal.h"
 
 namespace rtclj {
@@ -58,6 +60,14 @@ struct alignas(16) KArgs {
   int width;
   int rows_out;
   int row_begin, row_tile, tile_first, tile_step;
+  // BVH traversal (SCAN_BVH): blob = nodes | pairs | pidx (the LDS image)
+  const float4* bvh_blob;
+  const int* bvh_big;    // bodies scanned before the traversal (ascending)
+  int bvh_blob_f4;       // blob size in float4
+  int bvh_off_pairs;     // byte offsets inside the blob
+  int bvh_off_pidx;
+  int n_big;
+  float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   int spp, sample_begin, max_depth;
   uint32_t key;
 };
@@ -96,7 +106,7 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
 
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
-enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3 };
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -104,6 +114,12 @@ struct alignas(16) Pair {
   f2 x, y, z, w;   // centres and -r^2 of bodies 2p and 2p+1
 };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// BVH node as the kernel reads it (= rtclj::BvhNode, bvh.h)
+struct alignas(16) KNode {
+  f2 minx, miny, minz, maxx, maxy, maxz;   // (child0, child1)
+  int c0, c1, pad0, pad1;
+};
 
 // Sample stripes (arithmetic contract): a pixel's spp samples are split into
 // P = min(4, spp) contiguous stripes (stripe s: samples [s*q + min(s,r),
@@ -126,11 +142,19 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if constexpr (SRC == SRC_LDS) {
+  if constexpr (SCAN == SCAN_BVH) {
+    if constexpr (SRC == SRC_LDS) {
+      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
+      __syncthreads();
+    }
+  } else if constexpr (SRC == SRC_LDS) {
     const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
     for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
     __syncthreads();
   }
+  // BVH traversal stack: kBvhStack node indices per lane, [entry][lane] (no bank conflicts)
+  unsigned short* s_stack = reinterpret_cast<unsigned short*>(
+      reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
 
   // lane -> (pixel, stripe group): a wave owns a TW x TH pixel tile
   // (PX = 64/LPP pixels), lane group grp = lane / PX; the block's 4 waves
@@ -262,6 +286,97 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
         if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) consider(h, disc, s);
       }
+    } else if constexpr (SCAN == SCAN_BVH) {
+      // Closest hit through the BVH (bvh.cpp), bit-identical to the scan:
+      //  * each body is tested by the scan's fp32 op sequence and accepted if
+      //    t is smaller, or equal with a lower index (= the scan's first-wins);
+      //  * boxes are padded per ray by P = 2e-3 * D, D = |O - c| + R bounding
+      //    |oc| + r of every tree body: the fp32 test never reports a point
+      //    farther than 6e-4 * (|oc| + r) outside a body's box (measured,
+      //    tools/pad_bound.cpp, 3x margin), so a body the scan would accept
+      //    always lies in every box on its path; a box is skipped only if its
+      //    padded interval misses (tmin, best_t].
+      auto consider_tie = [&](float h, float disc, int s) {
+        if constexpr (STATS) ++st_blk_lanes;
+        const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
+        float t = h - sq;
+        if (!(t > tmin)) t = h + sq;
+        if (t > tmin && (t < best_t || (t == best_t && s < best))) {
+          best_t = t;
+          best = s;
+        }
+      };
+      // 1) big bodies (kept out of the tree), ascending index
+      for (int i = 0; i < a.n_big; ++i) {
+        const int s = a.bvh_big[i];
+        const float4 g = a.geo[s];
+        const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
+        const float h = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
+        const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
+        const float disc = fmaf(h, h, -c);
+        if (fminf(disc, fmaxf(h, -c)) >= 0.0f) consider_tie(h, disc, s);
+      }
+      // 2) the tree
+      const char* base = SRC == SRC_LDS ? reinterpret_cast<const char*>(s_geo)
+                                        : reinterpret_cast<const char*>(a.bvh_blob);
+      const KNode* nodes = reinterpret_cast<const KNode*>(base);
+      const Pair* pairs = reinterpret_cast<const Pair*>(base + a.bvh_off_pairs);
+      const int2* pidx = reinterpret_cast<const int2*>(base + a.bvh_off_pidx);
+      const float ecx = ox - a.bvh_c[0], ecy = oy - a.bvh_c[1], ecz = oz - a.bvh_c[2];
+      const float D = sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
+      const float P = fmaf(2e-3f, D, 1e-6f);
+      const f2 ix2 = {1.0f / ux, 1.0f / ux}, iy2 = {1.0f / uy, 1.0f / uy}, iz2 = {1.0f / uz, 1.0f / uz};
+      const f2 lox = {ox + P, ox + P}, loy = {oy + P, oy + P}, loz = {oz + P, oz + P};
+      const f2 hix = {ox - P, ox - P}, hiy = {oy - P, oy - P}, hiz = {oz - P, oz - P};
+      const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
+      const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
+      auto leaf = [&](int p) {
+        if constexpr (STATS) ++st_blk;
+        const Pair g = pairs[p];
+        const int2 id = pidx[p];
+        const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
+        const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
+        const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
+        const f2 disc = fma2(h, h, -c);
+        if (fminf(disc.x, fmaxf(h.x, -c.x)) >= 0.0f) consider_tie(h.x, disc.x, id.x);
+        if (fminf(disc.y, fmaxf(h.y, -c.y)) >= 0.0f) consider_tie(h.y, disc.y, id.y);
+      };
+      int node = 0, sp = 0;
+      for (;;) {
+        if constexpr (STATS) ++st_sph;
+        const KNode nd = nodes[node];
+        const f2 t1x = (nd.minx - lox) * ix2, t2x = (nd.maxx - hix) * ix2;
+        const f2 t1y = (nd.miny - loy) * iy2, t2y = (nd.maxy - hiy) * iy2;
+        const f2 t1z = (nd.minz - loz) * iz2, t2z = (nd.maxz - hiz) * iz2;
+        const float tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
+        const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
+        const float tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
+        const float tf1 = fminf(fminf(fmaxf(t1x.y, t2x.y), fmaxf(t1y.y, t2y.y)), fmaxf(t1z.y, t2z.y));
+        bool hit0 = (nd.c0 != INT_MIN) & (tn0 <= tf0) & (tf0 >= tmin) & (tn0 <= best_t);
+        bool hit1 = (nd.c1 != INT_MIN) & (tn1 <= tf1) & (tf1 >= tmin) & (tn1 <= best_t);
+        if (hit0 && nd.c0 < 0) {
+          leaf(~nd.c0);
+          hit0 = false;
+        }
+        if (hit1 && nd.c1 < 0) {
+          leaf(~nd.c1);
+          hit1 = false;
+        }
+        if (hit0 && hit1) {
+          const bool sw = tn1 < tn0;
+          s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? nd.c0 : nd.c1);
+          ++sp;
+          node = sw ? nd.c1 : nd.c0;
+        } else if (hit0) {
+          node = nd.c0;
+        } else if (hit1) {
+          node = nd.c1;
+        } else {
+          if (sp == 0) break;
+          --sp;
+          node = s_stack[sp * 256 + threadIdx.x];
+        }
+      }
     } else if constexpr (SCAN == SCAN_PK4) {
       // As SCAN_GROUP4, but the arithmetic of two bodies runs in one packed
       // instruction (v_pk_add/mul/fma_f32: each half is the same IEEE-rounded
@@ -334,7 +449,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         g3 = n3;
       }
     }
-    if constexpr (STATS) {
+    if constexpr (STATS && SCAN != SCAN_BVH) {
       const uint64_t ex = __builtin_amdgcn_read_exec();
       if (lane == __ffsll(static_cast<long long>(ex)) - 1) st_sph += static_cast<uint64_t>(n);
     }
@@ -499,8 +614,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     if (a.dbg && st_iter) {
       atomicAdd(&a.dbg[0], static_cast<unsigned long long>(st_iter));
       atomicAdd(&a.dbg[1], static_cast<unsigned long long>(st_lanes));
-      atomicAdd(&a.dbg[2], static_cast<unsigned long long>(st_sph));
     }
+    if (a.dbg && st_sph) atomicAdd(&a.dbg[2], static_cast<unsigned long long>(st_sph));
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
@@ -537,7 +652,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 //   3 = 1 + stats                   4 LDS table, grouped scan (prefetch)
 //   5 scalar, grouped scan          6 = 4 + stats        7 = 5 + stats
 //   8 LDS table, packed pairs      9 scalar, packed pairs   10 = 9 + stats
-//   0 = default (5)
+//  11 BVH in LDS                  12 BVH in global memory   13 = 11 + stats
+//     (BVH variants fall back to 5 when the tree does not fit / is too deep)
+//   0 = default (11)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
 // 0 = automatic (enough waves to keep the chip full to the end).
 struct Variant {
@@ -547,9 +664,9 @@ struct Variant {
 };
 #define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
 static const Variant& variant_table(int v) {
-  static const Variant t[11] = {
-      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, false), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, false),
-        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, false)}, false, false},
+  static const Variant t[14] = {
+      {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
+        RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
       {{RT_K(SRC_SCALAR, SCAN_SIMPLE, 1, false), nullptr, nullptr}, false, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, true), nullptr, nullptr}, true, true},
@@ -567,8 +684,14 @@ static const Variant& variant_table(int v) {
         RT_K(SRC_SCALAR, SCAN_PK4, 4, false)}, false, false},
       {{RT_K(SRC_SCALAR, SCAN_PK4, 1, true), RT_K(SRC_SCALAR, SCAN_PK4, 2, true),
         RT_K(SRC_SCALAR, SCAN_PK4, 4, true)}, false, true},
+      {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
+        RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
+      {{RT_K(SRC_SCALAR, SCAN_BVH, 1, false), RT_K(SRC_SCALAR, SCAN_BVH, 2, false),
+        RT_K(SRC_SCALAR, SCAN_BVH, 4, false)}, false, false},
+      {{RT_K(SRC_LDS, SCAN_BVH, 1, true), RT_K(SRC_LDS, SCAN_BVH, 2, true),
+        RT_K(SRC_LDS, SCAN_BVH, 4, true)}, true, true},
   };
-  return t[(v >= 0 && v < 11) ? v : 0];
+  return t[(v >= 0 && v < 14) ? v : 0];
 }
 #undef RT_K
 static int g_lpp = 0;  // 0 = automatic
@@ -599,6 +722,11 @@ struct rt_dscene {
   int n_pad;
   float4* geo;
   float4* geo2;   // n_pad/2 Pairs (= n_pad float4)
+  // BVH (bvh.cpp): device blob nodes | pairs | pidx and the big-body list
+  float4* bvh_blob;
+  int* bvh_big;
+  int bvh_blob_f4, bvh_off_pairs, bvh_off_pidx, n_big, bvh_depth;
+  float bvh_c[3], bvh_r;
   float4* sph;
   float4* mat;
   int* kind;
@@ -616,7 +744,7 @@ static int hip_fail(hipError_t e, const char* what) {
 
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
-  if (v >= 0 && v <= 10) g_variant = v;
+  if (v >= 0 && v <= 13) g_variant = v;
   return old;
 }
 
@@ -671,8 +799,34 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     o[0] = b0.x; o[1] = b1.x; o[2] = b0.y; o[3] = b1.y;
     o[4] = b0.z; o[5] = b1.z; o[6] = b0.w; o[7] = b1.w;
   }
-  rt_dscene* d = new rt_dscene{device, n, n_pad, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // BVH over the bodies (the traversal variants): blob = nodes | pairs | pidx
+  BvhHost bvh;
+  bvh_build(s->sphere, n, &bvh);
+  const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
+  const size_t pb = bvh.pairs.size() * sizeof(float);
+  const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;
+  std::vector<char> blob(nb + pb + ib, 0);
+  std::memcpy(blob.data(), bvh.nodes.data(), nb);
+  std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
+  std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
+  std::vector<int> big = bvh.big;
+  if (big.empty()) big.push_back(0);
+  rt_dscene* d = new rt_dscene{};
+  d->device = device;
+  d->n = n;
+  d->n_pad = n_pad;
+  d->bvh_blob_f4 = static_cast<int>(blob.size() / 16);
+  d->bvh_off_pairs = static_cast<int>(nb);
+  d->bvh_off_pidx = static_cast<int>(nb + pb);
+  d->n_big = static_cast<int>(bvh.big.size());
+  d->bvh_depth = bvh.depth;
+  for (int k = 0; k < 3; ++k) d->bvh_c[k] = bvh.center[k];
+  d->bvh_r = bvh.radius;
   hipError_t e = hipMalloc(&d->geo, n_pad * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&d->bvh_blob, blob.size());
+  if (e == hipSuccess) e = hipMemcpy(d->bvh_blob, blob.data(), blob.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&d->bvh_big, big.size() * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpy(d->bvh_big, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&d->geo2, n_pad * sizeof(float4));
   if (e == hipSuccess) e = hipMemcpy(d->geo2, geo2.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&d->sph, cnt * sizeof(float4));
@@ -695,6 +849,8 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   (void)hipSetDevice(d->device);
   if (d->geo) (void)hipFree(d->geo);
   if (d->geo2) (void)hipFree(d->geo2);
+  if (d->bvh_blob) (void)hipFree(d->bvh_blob);
+  if (d->bvh_big) (void)hipFree(d->bvh_big);
   if (d->sph) (void)hipFree(d->sph);
   if (d->mat) (void)hipFree(d->mat);
   if (d->kind) (void)hipFree(d->kind);
@@ -713,6 +869,14 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   KArgs a{};
   a.geo = ds->geo;
   a.geo2 = reinterpret_cast<const Pair*>(ds->geo2);
+  a.bvh_blob = ds->bvh_blob;
+  a.bvh_big = ds->bvh_big;
+  a.bvh_blob_f4 = ds->bvh_blob_f4;
+  a.bvh_off_pairs = ds->bvh_off_pairs;
+  a.bvh_off_pidx = ds->bvh_off_pidx;
+  a.n_big = ds->n_big;
+  for (int k = 0; k < 3; ++k) a.bvh_c[k] = ds->bvh_c[k];
+  a.bvh_r = ds->bvh_r;
   a.sph = ds->sph;
   a.mat = ds->mat;
   a.kind = ds->kind;
@@ -739,7 +903,16 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
-  const Variant& v = variant_table(g_variant);
+  int vsel = g_variant;
+  const size_t stack_bytes = static_cast<size_t>(kBvhStack) * 256 * sizeof(unsigned short);
+  const size_t bvh_lds = static_cast<size_t>(ds->bvh_blob_f4) * 16 + stack_bytes;
+  if (vsel == 0) vsel = 11;
+  if (vsel >= 11 && vsel <= 13) {
+    if (ds->bvh_depth > kBvhStack) vsel = 5;                   // tree too deep for the stack
+    else if (vsel != 12 && bvh_lds > 96 * 1024) vsel = 12;      // tree too big for LDS
+  }
+  const Variant& v = variant_table(vsel);
+  const bool is_bvh = vsel >= 11 && vsel <= 13;
   const int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr);
   const int tw = lpp == 4 ? 4 : 8, th = lpp == 1 ? 8 : 4;   // wave tile (trace_kernel)
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
@@ -757,7 +930,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     a.dbgw = g_dbgw;
   }
   size_t lds = 0;
-  if (v.lds) {
+  if (is_bvh) {
+    lds = v.lds ? bvh_lds : stack_bytes;
+    if (lds > 64 * 1024)
+      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  } else if (v.lds) {
     lds = static_cast<size_t>(ds->n_pad) * sizeof(float4);
     if (lds > 64 * 1024)
       HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));

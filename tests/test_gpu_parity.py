@@ -161,7 +161,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("lpp", [1, 2, 4])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
@@ -176,7 +176,7 @@ def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     try:
         st = {}
         g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7, 10):
+        if variant in (3, 6, 7, 10, 13):
             import ctypes as C
             d = (C.c_uint64 * 8)()
             lib.rt_debug_stats(d)
@@ -278,3 +278,27 @@ def test_c1_frame_properties(gpu_lib):
     assert 2.5 < st["segments"] / st["samples"] < 2.9
     ref, _, _ = _mirror(sc, cam, 1200, 675, 100, 50, seed=1, rows=(300, 302))
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
+
+
+@pytest.mark.parametrize("variant", [11, 12])
+def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
+    """The BVH traversal returns the scan's hits bit for bit: full C1 frame
+    (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import lib
+    cases = [(scenes.cover(11), scenes.cover_camera(1200, 675), 1200, 675, 100),
+             (scenes.cover(16), scenes.cover_camera(640, 360), 640, 360, 16),
+             (_ref_scene(), R.camera(400, 225, **R.REFERENCE_CAMERA), 400, 225, 100)]
+    for sc, cam, w, h, spp in cases:
+        old = lib.rt_set_variant(5)
+        try:
+            st_a = {}
+            a = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_a)
+            lib.rt_set_variant(variant)
+            st_b = {}
+            b = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_b)
+        finally:
+            lib.rt_set_variant(old)
+        assert np.array_equal(a, b), (w, h, int((a != b).any(axis=-1).sum()))
+        assert st_a["segments"] == st_b["segments"]

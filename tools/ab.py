@@ -58,7 +58,7 @@ def main():
             elif not np.array_equal(img, ref):
                 print(f"variant {name}: frame differs from variant {names[0]}!", flush=True)
                 sys.exit(1)
-            if v in (3, 6, 7, 10):
+            if v in (3, 6, 7, 10, 13):
                 d = (C.c_uint64 * 8)()
                 check(lib.rt_debug_stats(d))
                 d = list(d)
@@ -79,6 +79,10 @@ def main():
     print(f"segments/sample {seg:.4f}")
     if "dbg" in stats:
         it, lanes, sph, blk, blk_lanes, waves = stats["dbg"][:6]
+        segs_total = stats[names[0]]["segments"]
+        if stats["dbg_variant"].split(":")[0] == "13":
+            print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
+                              "bvh_considers_per_segment": blk_lanes / segs_total}))
         info = {"wave_iters": it, "simd_eff_loop": lanes / (64 * it), "iters_per_wave": it / waves,
                 "block_rate": blk / max(sph, 1), "lanes_per_block": blk_lanes / max(blk, 1), "waves": waves}
         wv = stats["waves"]
