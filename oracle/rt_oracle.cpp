@@ -17,7 +17,8 @@
 //       src/hit.clj:14-15, src/ray.clj:7-8
 //   MODE_MIRROR32 (1) — the GPU kernel's fp32 arithmetic contract
 //     (raytracing-clj_amd/csrc/trace.hip) restated op for op:
-//     explicit fmaf, correctly rounded / and sqrt, unit-direction hit test,
+//     explicit fmaf, correctly rounded / and sqrt, normalisation by one
+//     reciprocal (v * (1/|v|), (p - C) * (1/r)), unit-direction hit test,
 //     stackless throughput, exact "both roots behind" pre-filter, samples
 //     summed in min(4, spp) contiguous stripes then ((s0+s1)+s2)+s3.  The
 //     GPU output must equal this bit for bit.
@@ -245,10 +246,10 @@ void random_unit32(Rng& s, float& x, float& y, float& z) {
     z = 2.0f * s.uf() - 1.0f;
     l2 = std::fmaf(z, z, std::fmaf(y, y, x * x));
   } while (!(l2 > 0.0f && l2 <= 1.0f));
-  const float len = std::sqrt(l2);
-  x = x / len;
-  y = y / len;
-  z = z / len;
+  const float il = 1.0f / std::sqrt(l2);
+  x = x * il;
+  y = y * il;
+  z = z * il;
 }
 
 // one sample of the stackless kernel loop; returns colour, adds segments
@@ -283,7 +284,8 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, int px, int gy,
     --rem;
     *segs += 1;
     const float len = std::sqrt(std::fmaf(dz, dz, std::fmaf(dy, dy, dx * dx)));
-    const float ux = dx / len, uy = dy / len, uz = dz / len;
+    const float il = 1.0f / len;
+    const float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;
     float best_t = INFINITY;
     int best = -1;
@@ -318,7 +320,8 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, int px, int gy,
     const float hx = std::fmaf(ux, best_t, ox);
     const float hy = std::fmaf(uy, best_t, oy);
     const float hz = std::fmaf(uz, best_t, oz);
-    float nx = (hx - sp[0]) / sp[3], ny = (hy - sp[1]) / sp[3], nz = (hz - sp[2]) / sp[3];
+    const float ir = 1.0f / sp[3];
+    float nx = (hx - sp[0]) * ir, ny = (hy - sp[1]) * ir, nz = (hz - sp[2]) * ir;
     const bool front = std::fmaf(dz, nz, std::fmaf(dy, ny, dx * nx)) < 0.0f;
     if (!front) {
       nx = -nx;

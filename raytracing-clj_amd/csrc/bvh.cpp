@@ -14,7 +14,8 @@
 //
 // Layout (device, all 16-byte aligned):
 //   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
-//                    slab tests, child refs: >= 0 node, < 0 leaf ~pair, INT_MIN empty
+//                    slab tests, child refs: >= 0 node, < 0 leaf ~pair (every
+//                    child is real: small trees repeat a leaf / use a pad leaf)
 //   pairs[n_pairs]   two bodies per leaf: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
 //                    a missing second body has w = +inf: never a candidate)
 //   pidx[n_pairs]    original indices of the two bodies (-1 for the pad)
@@ -163,12 +164,18 @@ int bvh_build(const float* sph, int n, BvhHost* out) {
   out->nodes.emplace_back();
   const int cnt = static_cast<int>(b.prim.size());
   Box b0, b1;
-  int c0 = INT_MIN, c1 = INT_MIN;
-  if (cnt > 0) {
+  int c0 = 0, c1 = 0;
+  if (cnt == 0) {
+    // no tree bodies: both children are one pad-only leaf (never a candidate)
+    c0 = c1 = b.leaf(0, 0, &b0);
+    for (int k = 0; k < 3; ++k) b0.lo[k] = b0.hi[k] = 0.0f;
+    b1 = b0;
+  } else {
     const int mid = cnt <= 2 ? cnt : ((cnt / 2 + 1) & ~1);
     // split the root by the same rule as build() (axis from centroid bounds)
     if (cnt <= 2) {
-      c0 = b.leaf(0, cnt, &b0);
+      c0 = c1 = b.leaf(0, cnt, &b0);   // the same leaf twice: a repeat test never wins a tie
+      b1 = b0;
     } else {
       Box cb;
       for (int i : b.prim)

@@ -9,7 +9,7 @@ namespace rtclj {
 struct alignas(16) BvhNode {
   float minx[2], miny[2], minz[2];
   float maxx[2], maxy[2], maxz[2];
-  int child[2];   // >= 0: node, < 0: ~leaf pair index, INT_MIN: empty
+  int child[2];   // >= 0: node, < 0: ~leaf pair index
   int pad[2];
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode layout");

@@ -27,7 +27,9 @@
 // oracle/rt_oracle.cpp, so GPU and CPU agree bit-for-bit): every fused
 // multiply-add is an explicit fmaf, the file is compiled with
 // -ffp-contract=off, division and sqrt are IEEE correctly rounded (HIP's
-// default), and no transcendental function is used.  See DESIGN.md §3.
+// default), normalisations multiply by one correctly rounded reciprocal
+// (d * (1/|d|), (p - C) * (1/r)), and no transcendental function is used.
+// See DESIGN.md §3.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -45,8 +47,8 @@ namespace rtclj {
 struct alignas(16) KArgs {
   const float4* geo;   // n_pad: cx, cy, cz, -r*r   (hit test)
   const struct Pair* geo2;  // n_pad/2: the same, two bodies interleaved per Pair
-  const float4* sph;   // n: cx, cy, cz, r      (hit record)
-  const float4* mat;   // n: albedo rgb, fuzz | refraction index
+  const float4* sph;   // n: cx, cy, cz, 1/r    (hit record)
+  const float4* mat;   // n: albedo rgb, fuzz | refraction index (dielectric: x = 1/eta)
   const int* kind;     // n: material kind
   float* out;          // rows_out x width x 3
   unsigned long long* counters;  // NULL or [segments, samples]
@@ -98,10 +100,10 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
     z = rng_sym(s);
     l2 = fmaf(z, z, fmaf(y, y, x * x));
   } while (!(l2 > 0.0f && l2 <= 1.0f));
-  const float len = sqrtf(l2);
-  x = x / len;
-  y = y / len;
-  z = z / len;
+  const float il = 1.0f / sqrtf(l2);   // contract: v * (1/|v|)
+  x = x * il;
+  y = y * il;
+  z = z * il;
 }
 
 // ------------------------------------------------------------- kernel ----
@@ -138,6 +140,7 @@ template <int SRC, int SCAN, int LPP, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   static_assert(LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel");
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
+  uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_t0 = 0;
   if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
@@ -248,7 +251,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     --rem;
     ++segs;
     const float len = sqrtf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
-    const float ux = dx / len, uy = dy / len, uz = dz / len;   // vec3a/unit
+    const float il = 1.0f / len;                              // vec3a/unit as d * (1/|d|)
+    const float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
     float best_t = INFINITY;
     int best = -1;
@@ -323,9 +327,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const Pair* pairs = reinterpret_cast<const Pair*>(base + a.bvh_off_pairs);
       const int2* pidx = reinterpret_cast<const int2*>(base + a.bvh_off_pidx);
       const float ecx = ox - a.bvh_c[0], ecy = oy - a.bvh_c[1], ecz = oz - a.bvh_c[2];
-      const float D = sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
+      // box tests only cull (conservatively): hardware sqrt / rcp (1 ulp) are
+      // far inside the padding
+      const float D = __builtin_amdgcn_sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
       const float P = fmaf(2e-3f, D, 1e-6f);
-      const f2 ix2 = {1.0f / ux, 1.0f / ux}, iy2 = {1.0f / uy, 1.0f / uy}, iz2 = {1.0f / uz, 1.0f / uz};
+      const float rux = __builtin_amdgcn_rcpf(ux), ruy = __builtin_amdgcn_rcpf(uy), ruz = __builtin_amdgcn_rcpf(uz);
+      const f2 ix2 = {rux, rux}, iy2 = {ruy, ruy}, iz2 = {ruz, ruz};
       const f2 lox = {ox + P, ox + P}, loy = {oy + P, oy + P}, loz = {oz + P, oz + P};
       const f2 hix = {ox - P, ox - P}, hiy = {oy - P, oy - P}, hiz = {oz - P, oz - P};
       const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
@@ -343,7 +350,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       };
       int node = 0, sp = 0;
       for (;;) {
-        if constexpr (STATS) ++st_sph;
+        if constexpr (STATS) {
+          ++st_sph;
+          const uint64_t ex = __builtin_amdgcn_read_exec();
+          if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+            ++st_trav;
+            st_trav_lanes += __popcll(ex);
+          }
+        }
         const KNode nd = nodes[node];
         const f2 t1x = (nd.minx - lox) * ix2, t2x = (nd.maxx - hix) * ix2;
         const f2 t1y = (nd.miny - loy) * iy2, t2y = (nd.maxy - hiy) * iy2;
@@ -352,8 +366,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
         const float tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
         const float tf1 = fminf(fminf(fmaxf(t1x.y, t2x.y), fmaxf(t1y.y, t2y.y)), fmaxf(t1z.y, t2z.y));
-        bool hit0 = (nd.c0 != INT_MIN) & (tn0 <= tf0) & (tf0 >= tmin) & (tn0 <= best_t);
-        bool hit1 = (nd.c1 != INT_MIN) & (tn1 <= tf1) & (tf1 >= tmin) & (tn1 <= best_t);
+        // [tn, tf] meets (tmin, best_t] (tmin < best_t always; a NaN bound only
+        // makes the test pass: conservative)
+        bool hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
+        bool hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
         if (hit0 && nd.c0 < 0) {
           leaf(~nd.c0);
           hit0 = false;
@@ -472,7 +488,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float hx = fmaf(ux, best_t, ox);
       const float hy = fmaf(uy, best_t, oy);
       const float hz = fmaf(uz, best_t, oz);
-      float nx = (hx - sp.x) / sp.w, ny = (hy - sp.y) / sp.w, nz = (hz - sp.z) / sp.w;
+      // outward normal (p - C) / r, as (p - C) * (1/r) with 1/r from the table
+      float nx = (hx - sp.x) * sp.w, ny = (hy - sp.y) * sp.w, nz = (hz - sp.z) * sp.w;
       const bool front = fmaf(dz, nz, fmaf(dy, ny, dx * nx)) < 0.0f;
       if (!front) {
         nx = -nx;
@@ -485,44 +502,47 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       oy = hy;
       oz = hz;
       last = best;
-      if (kind == RT_LAMBERTIAN) {
-        // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
-        float rx, ry, rz;
-        random_unit(st, rx, ry, rz);
-        float sx = rx + nx, sy = ry + ny, sz = rz + nz;
-        if (fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {
-          sx = nx;
-          sy = ny;
-          sz = nz;
-        }
-        dx = sx;
-        dy = sy;
-        dz = sz;
-        tr *= m.x;
-        tg *= m.y;
-        tb *= m.z;
-      } else if (kind == RT_METAL) {
-        // material.clj:21-28: reflect the *un-normalised* d, add fuzz*unit
-        const float k2 = 2.0f * fmaf(dz, nz, fmaf(dy, ny, dx * nx));
-        const float rx0 = fmaf(-nx, k2, dx), ry0 = fmaf(-ny, k2, dy), rz0 = fmaf(-nz, k2, dz);
+      if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
+        // one random-unit-vec3 draw for either material (the only draws of
+        // the segment for these lanes): a wave loops the rejection sampler
+        // once for both kinds
         float qx, qy, qz;
         random_unit(st, qx, qy, qz);
-        const float rx = fmaf(m.w, qx, rx0), ry = fmaf(m.w, qy, ry0), rz = fmaf(m.w, qz, rz0);
-        if (fmaf(rz, nz, fmaf(ry, ny, rx * nx)) > 0.0f) {
-          dx = rx;
-          dy = ry;
-          dz = rz;
+        if (kind == RT_LAMBERTIAN) {
+          // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
+          float sx = qx + nx, sy = qy + ny, sz = qz + nz;
+          if (fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {
+            sx = nx;
+            sy = ny;
+            sz = nz;
+          }
+          dx = sx;
+          dy = sy;
+          dz = sz;
           tr *= m.x;
           tg *= m.y;
           tb *= m.z;
         } else {
-          done = true;  // absorbed: scatter-fn nil -> black (:51-54)
+          // material.clj:21-28: reflect the *un-normalised* d, add fuzz*unit
+          const float k2 = 2.0f * fmaf(dz, nz, fmaf(dy, ny, dx * nx));
+          const float rx0 = fmaf(-nx, k2, dx), ry0 = fmaf(-ny, k2, dy), rz0 = fmaf(-nz, k2, dz);
+          const float rx = fmaf(m.w, qx, rx0), ry = fmaf(m.w, qy, ry0), rz = fmaf(m.w, qz, rz0);
+          if (fmaf(rz, nz, fmaf(ry, ny, rx * nx)) > 0.0f) {
+            dx = rx;
+            dy = ry;
+            dz = rz;
+            tr *= m.x;
+            tg *= m.y;
+            tb *= m.z;
+          } else {
+            done = true;  // absorbed: scatter-fn nil -> black (:51-54)
+          }
         }
       } else if (kind == RT_NONE) {
         done = true;  // no ::scatter-fn -> black (raytracing.clj:49-54)
       } else {
         // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
-        const float ri = front ? (1.0f / m.w) : m.w;
+        const float ri = front ? m.x : m.w;   // 1/eta (host-divided) : eta
         const float un = fmaf(uz, nz, fmaf(uy, ny, ux * nx));
         const float cosv = fminf(-un, 1.0f);
         const float sinv = sqrtf(fmaf(-cosv, cosv, 1.0f));
@@ -616,6 +636,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[1], static_cast<unsigned long long>(st_lanes));
     }
     if (a.dbg && st_sph) atomicAdd(&a.dbg[2], static_cast<unsigned long long>(st_sph));
+    if (a.dbg && st_trav) {
+      atomicAdd(&a.dbg[6], static_cast<unsigned long long>(st_trav));
+      atomicAdd(&a.dbg[7], static_cast<unsigned long long>(st_trav_lanes));
+    }
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
@@ -786,9 +810,10 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     const float* q = s->sphere + 4 * i;
     const float r = q[3];
     geo[i] = make_float4(q[0], q[1], q[2], -(r * r));
-    sph[i] = make_float4(q[0], q[1], q[2], r);
+    sph[i] = make_float4(q[0], q[1], q[2], 1.0f / r);                   // 1/r for the normal
     const float* m = s->mat + 4 * i;
     mat[i] = make_float4(m[0], m[1], m[2], m[3]);
+    if (s->mat_kind[i] == RT_DIELECTRIC) mat[i].x = 1.0f / m[3];       // 1/eta (albedo unused)
     kind[i] = s->mat_kind[i];
   }
   // pair-interleaved copy for the packed scan: (x0 x1 y0 y1 z0 z1 w0 w1) per pair

@@ -81,8 +81,11 @@ def main():
         it, lanes, sph, blk, blk_lanes, waves = stats["dbg"][:6]
         segs_total = stats[names[0]]["segments"]
         if stats["dbg_variant"].split(":")[0] == "13":
+            tw, tl = stats["dbg"][6], stats["dbg"][7]
             print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
-                              "bvh_considers_per_segment": blk_lanes / segs_total}))
+                              "bvh_considers_per_segment": blk_lanes / segs_total,
+                              "trav_wave_iters_per_wave_iter": tw / it, "trav_lane_eff": tl / max(64 * tw, 1),
+                              "trav_lanes_active_frac_of_loop_lanes": tl / max(tw * (lanes / it), 1)}))
         info = {"wave_iters": it, "simd_eff_loop": lanes / (64 * it), "iters_per_wave": it / waves,
                 "block_rate": blk / max(sph, 1), "lanes_per_block": blk_lanes / max(blk, 1), "waves": waves}
         wv = stats["waves"]
