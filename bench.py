@@ -44,6 +44,11 @@ from rtclj._lib import check, lib, rt_params  # noqa: E402
 from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
 METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
+# executed fp32 flops (fma = 2) of the BVH traversal, per event:
+# node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
+# exact body test (sqrt, root choice) = 4; big-body scan test = 16
+FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v11"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -101,6 +106,42 @@ def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
             "host": platform.node()}
 
 
+def bvh_counters(ds, cam, p, out, counters, sh):
+    """One untimed launch of the stats build (variant 13) of the same frame:
+    per-segment node visits, leaf-pair tests, exact tests (rt_debug_stats)."""
+    old = lib.rt_set_variant(13)
+    try:
+        dbg = (C.c_uint64 * 16)()
+        check(lib.rt_debug_stats(dbg))                  # clear
+        counters.zero_()
+        check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()),
+                            C.c_void_p(counters.data_ptr()), sh))
+        torch.cuda.synchronize()
+        check(lib.rt_debug_stats(dbg))
+        segs = float(counters[0].item())
+    finally:
+        lib.rt_set_variant(old)
+    return {"nodes": dbg[2] / segs, "leaf_pairs": dbg[3] / segs, "exact_tests": dbg[4] / segs}
+
+
+def pmc_traffic(kernel_substr="trace_kernel"):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (separate
+    FETCH_SIZE / WRITE_SIZE runs, KB units; gfx950 FETCH_SIZE counts half the
+    bytes of wide streaming reads -> x2, MI355X_MICROARCH.md §HBM)."""
+    import csv
+    vals = {}
+    for name in ("fetch", "write"):
+        f = PMC_DEFAULT / f"{name}.csv"
+        if not f.exists():
+            return None, None
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
+             if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE")]
+        if not v:
+            return None, None
+        vals[name] = sum(v) / len(v) * 1024.0
+    return 2.0 * vals["fetch"] + vals["write"], str(PMC_DEFAULT.relative_to(ROOT))
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,12 +151,32 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     if a.gpus > 1 and world == 1:
         raise SystemExit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
-    if not torch.cuda.is_available() or lib.rt_device_count() <= 0:
+    ndev = lib.rt_device_count()
+    if not torch.cuda.is_available() or ndev <= 0:
         raise SystemExit("bench.py needs a GPU (MI355X); no device visible")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; more ranks than GPUs only for rehearsals (ranks share)
+    device = local % ndev
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
+    # The render exchanges nothing between ranks (pixels/samples are
+    # independent; RNG keyed by (seed, pixel, sample)): the only cross-rank
+    # traffic is the barrier and the max/sum of three timing scalars, done on
+    # the host over gloo (BENCH_DIST_BACKEND=nccl moves them to RCCL).
+    backend = os.environ.get("BENCH_DIST_BACKEND", "gloo")
     if world > 1:
-        dist.init_process_group(backend=os.environ.get("BENCH_DIST_BACKEND", "nccl"))
+        # C-level banners (gloo prints "connected to N peer ranks") go to
+        # stderr: stdout carries exactly one JSON line
+        saved = os.dup(1)
+        sys.stdout.flush()
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend=backend)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
     lib.rt_set_variant(a.variant)
     lib.rt_set_lanes_per_pixel(a.lpp)
 
@@ -129,7 +190,7 @@ def main():
     cam = scenes.cover_camera(W, H)
 
     ds = C.c_void_p()
-    check(lib.rt_scene_upload(local, C.byref(scene.c), C.byref(ds)))
+    check(lib.rt_scene_upload(device, C.byref(scene.c), C.byref(ds)))
     p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
     rows = check(lib.rt_rows_out(C.byref(p)))
     assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
@@ -167,12 +228,13 @@ def main():
     local_stats = torch.tensor([elapsed, max(kern_ms), sum(kern_ms) / len(kern_ms)], dtype=torch.float64)
     tot = torch.tensor([float(cnt[0]), float(cnt[1])], dtype=torch.float64)
     if world > 1:
-        ls, tt = local_stats.to(dev), tot.to(dev)
+        ls, tt = local_stats.to(red_dev), tot.to(red_dev)
         dist.all_reduce(ls, op=dist.ReduceOp.MAX)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         local_stats, tot = ls.cpu(), tt.cpu()
     elapsed, kern_max_ms, kern_avg_ms = local_stats.tolist()
     segs_total, samples_total = tot.tolist()
+    bvh = bvh_counters(ds, cam, p, out, counters, sh) if rank == 0 and a.variant in (0, 11, 13) else None
     lib.rt_scene_free(ds)
 
     if rank == 0:
@@ -182,10 +244,21 @@ def main():
         # dominant kernel, per launch on this rank (rank-0 share at N>1)
         launch_samples = rows * W * spp
         launch_segs = seg_per_sample * launch_samples
-        flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT)
-        tflops = flops / (kern_avg_ms * 1e-3) / 1e12
+        bf_flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT)
+        bf_tflops = bf_flops / (kern_avg_ms * 1e-3) / 1e12
+        if bvh is not None:
+            per_seg = (FLOPS_NODE * bvh["nodes"] + FLOPS_LEAF_PAIR * bvh["leaf_pairs"] +
+                       FLOPS_EXACT * bvh["exact_tests"] + FLOPS_BODY * 1 + FLOPS_PER_SEGMENT)
+            work = (f"BVH traversal, executed fp32 work per segment = 24 x {bvh['nodes']:.2f} nodes + "
+                    f"32 x {bvh['leaf_pairs']:.2f} leaf pairs + 4 x {bvh['exact_tests']:.2f} exact tests + "
+                    f"16 (ground) + 100 = {per_seg:.0f} flops (counters: one untimed stats launch)")
+        else:
+            per_seg = FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT
+            work = f"linear scan, executed fp32 work per segment = 17 x {len(scene)} bodies + 100"
+        tflops = launch_segs * per_seg / (kern_avg_ms * 1e-3) / 1e12
         hbm_bytes = rows * W * 12 + len(scene) * 32
         gbs = hbm_bytes / (kern_avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic()
         res = {
             "metric": METRIC, "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -197,15 +270,18 @@ def main():
                        "parallelism": ("sample-stripe x%d (weak)" % world) if a.scaling == "weak"
                        else ("row-tile 8 x%d (strong)" % world), "variant": a.variant},
             "roofline": {"bound": "valu", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tflops / PEAK_FP32_TFLOPS, "traffic": None,
-                         "note": f"fp32 VALU (no MFMA: branchy scalar FP). algorithmic flops/launch = segments "
-                                 f"x (17 x {len(scene)} bodies + 100); peak = fp32 vector peak"},
+                         "frac": tflops / PEAK_FP32_TFLOPS, "traffic": traffic,
+                         "note": f"fp32 VALU (no MFMA: branchy scalar FP); {work}; peak = fp32 vector peak. "
+                                 f"Brute-force-equivalent (SURVEY §8d: 17 x {len(scene)} + 100 per segment): "
+                                 f"{bf_tflops:.1f} TF/s. traffic = HBM bytes/launch from {traffic_src} "
+                                 f"(FETCH x2 + WRITE)"},
             "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+                             "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
+            "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
-            "kernel": "rtclj::trace_kernel<%d>" % (2 if a.variant == 2 else 1),
+            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = BVH in LDS, 4 lanes/pixel)" % a.variant,
             "cpu_baseline": None,
         }
         if a.cpu_baseline == "auto" and world == 1:

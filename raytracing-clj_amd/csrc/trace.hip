@@ -106,9 +106,25 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
   z = z * il;
 }
 
+// stats build only: shader-clock stamp (s_memtime, drains lgkm; diagnostic)
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), off);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), off);
+    const uint64_t o = (static_cast<uint64_t>(hi) << 32) | lo;
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
-enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4 };
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -141,11 +157,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   static_assert(LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel");
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
+  uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if constexpr (SCAN == SCAN_BVH) {
+  if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVHWW) {
     if constexpr (SRC == SRC_LDS) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
       __syncthreads();
@@ -207,6 +224,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   bool fresh = true;
 
   while (active) {
+    if constexpr (STATS) st_ts = stamp();
     if constexpr (STATS) {  // counted once per wave event, by its first active lane
       const uint64_t ex = __builtin_amdgcn_read_exec();
       if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -247,6 +265,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       fresh = false;
     }
 
+    if constexpr (STATS) {
+      const uint64_t t = stamp();
+      st_c_cam += t - st_ts;
+      st_ts = t;
+    }
     // ---- one ray-color level: hit-anything over all bodies ----
     --rem;
     ++segs;
@@ -290,7 +313,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
         if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) consider(h, disc, s);
       }
-    } else if constexpr (SCAN == SCAN_BVH) {
+    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVHWW) {
       // Closest hit through the BVH (bvh.cpp), bit-identical to the scan:
       //  * each body is tested by the scan's fp32 op sequence and accepted if
       //    t is smaller, or equal with a lower index (= the scan's first-wins);
@@ -348,6 +371,85 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         if (fminf(disc.x, fmaxf(h.x, -c.x)) >= 0.0f) consider_tie(h.x, disc.x, id.x);
         if (fminf(disc.y, fmaxf(h.y, -c.y)) >= 0.0f) consider_tie(h.y, disc.y, id.y);
       };
+      // slab test of both children of node nd: entry/exit t and the cull
+      // predicate "[tn, tf] meets (tmin, best_t]" (tmin < best_t always; a NaN
+      // bound only makes the test pass: conservative)
+      auto node_test = [&](const KNode& nd, float& tn0, float& tn1, bool& hit0, bool& hit1) {
+        const f2 t1x = (nd.minx - lox) * ix2, t2x = (nd.maxx - hix) * ix2;
+        const f2 t1y = (nd.miny - loy) * iy2, t2y = (nd.maxy - hiy) * iy2;
+        const f2 t1z = (nd.minz - loz) * iz2, t2z = (nd.maxz - hiz) * iz2;
+        tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
+        const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
+        tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
+        const float tf1 = fminf(fminf(fmaxf(t1x.y, t2x.y), fmaxf(t1y.y, t2y.y)), fmaxf(t1z.y, t2z.y));
+        hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
+        hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
+      };
+      if constexpr (SCAN == SCAN_BVHWW) {
+        // speculative while-while (Aila & Laine 2009): a node phase in which
+        // a lane that already holds a leaf keeps descending until every lane
+        // holds one (or has run out of nodes), then one leaf phase in which
+        // the lanes test their leaves together -- the wave no longer runs the
+        // leaf test for a few lanes at every node step.  Stack entries are
+        // child refs (node >= 0, leaf ~p < 0); at most depth + 2 are live.
+        short* stk = reinterpret_cast<short*>(s_stack);
+        int node = 0, pend = -1, sp = 0;
+        for (;;) {
+          while (node >= 0) {
+            if constexpr (STATS) {
+              ++st_sph;
+              const uint64_t ex = __builtin_amdgcn_read_exec();
+              if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+                ++st_trav;
+                st_trav_lanes += __popcll(ex);
+              }
+            }
+            const KNode nd = nodes[node];
+            float tn0, tn1;
+            bool hit0, hit1;
+            node_test(nd, tn0, tn1, hit0, hit1);
+            const bool sw = tn1 < tn0;   // near child first
+            const int cn = sw ? nd.c1 : nd.c0, cf = sw ? nd.c0 : nd.c1;
+            const bool hn = sw ? hit1 : hit0, hf = sw ? hit0 : hit1;
+            int next = -1;
+            if (hf) {       // far child: pushed unless it is the only way on
+              if (cf < 0 && pend < 0 && !(hn && cn < 0)) pend = ~cf;
+              else if (cf >= 0 && !hn) next = cf;
+              else stk[(sp++) * 256 + threadIdx.x] = static_cast<short>(cf);
+            }
+            if (hn) {
+              if (cn < 0) {
+                if (pend < 0) pend = ~cn;
+                else stk[(sp++) * 256 + threadIdx.x] = static_cast<short>(cn);
+              } else {
+                next = cn;
+              }
+            }
+            node = next;
+            if (node < 0) {
+              if (pend >= 0 || sp == 0) break;       // test the leaf first / done
+              const int e = stk[(--sp) * 256 + threadIdx.x];
+              if (e >= 0) {
+                node = e;
+              } else {
+                pend = ~e;
+                break;
+              }
+            }
+            if (__all(pend >= 0)) break;             // every lane holds a leaf
+          }
+          if (pend >= 0) {
+            leaf(pend);
+            pend = -1;
+          }
+          if (node < 0) {
+            if (sp == 0) break;
+            const int e = stk[(--sp) * 256 + threadIdx.x];
+            if (e >= 0) node = e;
+            else pend = ~e;
+          }
+        }
+      } else {
       int node = 0, sp = 0;
       for (;;) {
         if constexpr (STATS) {
@@ -392,6 +494,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           --sp;
           node = s_stack[sp * 256 + threadIdx.x];
         }
+      }
       }
     } else if constexpr (SCAN == SCAN_PK4) {
       // As SCAN_GROUP4, but the arithmetic of two bodies runs in one packed
@@ -465,11 +568,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         g3 = n3;
       }
     }
-    if constexpr (STATS && SCAN != SCAN_BVH) {
+    if constexpr (STATS && SCAN != SCAN_BVH && SCAN != SCAN_BVHWW) {
       const uint64_t ex = __builtin_amdgcn_read_exec();
       if (lane == __ffsll(static_cast<long long>(ex)) - 1) st_sph += static_cast<uint64_t>(n);
     }
 
+    if constexpr (STATS) {
+      const uint64_t t = stamp();
+      st_c_scan += t - st_ts;
+      st_ts = t;
+    }
     bool done = false;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     if (best < 0) {
@@ -573,6 +681,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       }
     }
 
+    if constexpr (STATS) {
+      const uint64_t t = stamp();
+      st_c_shade += t - st_ts;
+      st_ts = t;
+    }
     if (done) {
       accr += cr;
       accg += cg;
@@ -598,6 +711,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       }
       if (k >= k_end) active = false;
     }
+    if constexpr (STATS) st_c_acc += stamp() - st_ts;
   }
 
   // ---- per-pixel total ((s0 + s1) + s2) + s3, / spp (raytracing.clj:155) ----
@@ -645,6 +759,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
     }
     if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+    // clock split: the lane active longest saw every iteration (max over lanes)
+    const uint64_t c0 = wave_max_u64(st_c_cam), c1 = wave_max_u64(st_c_scan);
+    const uint64_t c2 = wave_max_u64(st_c_shade), c3 = wave_max_u64(st_c_acc);
+    if (a.dbg && lane == 0) {
+      atomicAdd(&a.dbg[8], static_cast<unsigned long long>(c0));
+      atomicAdd(&a.dbg[9], static_cast<unsigned long long>(c1));
+      atomicAdd(&a.dbg[10], static_cast<unsigned long long>(c2));
+      atomicAdd(&a.dbg[11], static_cast<unsigned long long>(c3));
+    }
     if (a.dbgw && lane == 0) {
       const size_t wid = (static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
       if (wid < 65536) {
@@ -677,6 +800,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 //   5 scalar, grouped scan          6 = 4 + stats        7 = 5 + stats
 //   8 LDS table, packed pairs      9 scalar, packed pairs   10 = 9 + stats
 //  11 BVH in LDS                  12 BVH in global memory   13 = 11 + stats
+//  14 BVH in LDS, speculative while-while traversal          15 = 14 + stats
 //     (BVH variants fall back to 5 when the tree does not fit / is too deep)
 //   0 = default (11)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
@@ -688,7 +812,7 @@ struct Variant {
 };
 #define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
 static const Variant& variant_table(int v) {
-  static const Variant t[14] = {
+  static const Variant t[16] = {
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
         RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
@@ -714,8 +838,12 @@ static const Variant& variant_table(int v) {
         RT_K(SRC_SCALAR, SCAN_BVH, 4, false)}, false, false},
       {{RT_K(SRC_LDS, SCAN_BVH, 1, true), RT_K(SRC_LDS, SCAN_BVH, 2, true),
         RT_K(SRC_LDS, SCAN_BVH, 4, true)}, true, true},
+      {{RT_K(SRC_LDS, SCAN_BVHWW, 1, false), RT_K(SRC_LDS, SCAN_BVHWW, 2, false),
+        RT_K(SRC_LDS, SCAN_BVHWW, 4, false)}, true, false},
+      {{RT_K(SRC_LDS, SCAN_BVHWW, 1, true), RT_K(SRC_LDS, SCAN_BVHWW, 2, true),
+        RT_K(SRC_LDS, SCAN_BVHWW, 4, true)}, true, true},
   };
-  return t[(v >= 0 && v < 14) ? v : 0];
+  return t[(v >= 0 && v < 16) ? v : 0];
 }
 #undef RT_K
 static int g_lpp = 0;  // 0 = automatic
@@ -768,7 +896,7 @@ static int hip_fail(hipError_t e, const char* what) {
 
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
-  if (v >= 0 && v <= 13) g_variant = v;
+  if (v >= 0 && v <= 15) g_variant = v;
   return old;
 }
 
@@ -932,12 +1060,12 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   const size_t stack_bytes = static_cast<size_t>(kBvhStack) * 256 * sizeof(unsigned short);
   const size_t bvh_lds = static_cast<size_t>(ds->bvh_blob_f4) * 16 + stack_bytes;
   if (vsel == 0) vsel = 11;
-  if (vsel >= 11 && vsel <= 13) {
-    if (ds->bvh_depth > kBvhStack) vsel = 5;                   // tree too deep for the stack
+  if (vsel >= 11 && vsel <= 15) {
+    if (ds->bvh_depth + 2 > kBvhStack) vsel = 5;               // tree too deep for the stack
     else if (vsel != 12 && bvh_lds > 96 * 1024) vsel = 12;      // tree too big for LDS
   }
   const Variant& v = variant_table(vsel);
-  const bool is_bvh = vsel >= 11 && vsel <= 13;
+  const bool is_bvh = vsel >= 11 && vsel <= 15;
   const int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr);
   const int tw = lpp == 4 ? 4 : 8, th = lpp == 1 ? 8 : 4;   // wave tile (trace_kernel)
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
@@ -946,8 +1074,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
   if (v.stats) {
     if (!g_dbg) {
-      HIP_TRY(hipMalloc(&g_dbg, 8 * sizeof(unsigned long long)));
-      HIP_TRY(hipMemset(g_dbg, 0, 8 * sizeof(unsigned long long)));
+      HIP_TRY(hipMalloc(&g_dbg, 16 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(g_dbg, 0, 16 * sizeof(unsigned long long)));
       HIP_TRY(hipMalloc(&g_dbgw, 4 * 65536 * sizeof(unsigned long long)));
       HIP_TRY(hipMemset(g_dbgw, 0, 4 * 65536 * sizeof(unsigned long long)));
     }
@@ -970,16 +1098,16 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   return RT_OK;
 }
 
-// Stats build (variant 3) read-back: copies and clears the 8 debug counters.
-extern "C" int rt_debug_stats(uint64_t* out8) {
-  if (!out8) return set_error(RT_E_ARG, "rt_debug_stats: NULL");
+// Stats builds read-back: copies and clears the 16 debug counters.
+extern "C" int rt_debug_stats(uint64_t* out16) {
+  if (!out16) return set_error(RT_E_ARG, "rt_debug_stats: NULL");
   if (!g_dbg) {
-    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    for (int i = 0; i < 16; ++i) out16[i] = 0;
     return RT_OK;
   }
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out8, g_dbg, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemset(g_dbg, 0, 8 * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpy(out16, g_dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(g_dbg, 0, 16 * sizeof(uint64_t)));
   return RT_OK;
 }
 

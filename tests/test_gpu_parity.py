@@ -161,7 +161,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("lpp", [1, 2, 4])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
@@ -176,9 +176,9 @@ def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     try:
         st = {}
         g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7, 10, 13):
+        if variant in (3, 6, 7, 10, 13, 15):
             import ctypes as C
-            d = (C.c_uint64 * 8)()
+            d = (C.c_uint64 * 16)()
             lib.rt_debug_stats(d)
     finally:
         lib.rt_set_variant(ov)
@@ -280,7 +280,7 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("variant", [11, 12])
+@pytest.mark.parametrize("variant", [11, 12, 14])
 def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""

@@ -58,8 +58,8 @@ def main():
             elif not np.array_equal(img, ref):
                 print(f"variant {name}: frame differs from variant {names[0]}!", flush=True)
                 sys.exit(1)
-            if v in (3, 6, 7, 10, 13):
-                d = (C.c_uint64 * 8)()
+            if v in (3, 6, 7, 10, 13, 15):
+                d = (C.c_uint64 * 16)()
                 check(lib.rt_debug_stats(d))
                 d = list(d)
                 stats["dbg"] = d
@@ -80,7 +80,7 @@ def main():
     if "dbg" in stats:
         it, lanes, sph, blk, blk_lanes, waves = stats["dbg"][:6]
         segs_total = stats[names[0]]["segments"]
-        if stats["dbg_variant"].split(":")[0] == "13":
+        if stats["dbg_variant"].split(":")[0] in ("13", "15"):
             tw, tl = stats["dbg"][6], stats["dbg"][7]
             print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
                               "bvh_considers_per_segment": blk_lanes / segs_total,
@@ -100,6 +100,10 @@ def main():
                     life_us_min=float(life.min()), resident_waves_over_time=occ,
                     max_resident=int(max(occ)), start_last_us=float(st_.max()),
                     distinct_cu_xcc=int(len(set(zip(cu.tolist(), xcc.tolist())))))
+        cyc = stats["dbg"][8:12]
+        tot = max(sum(cyc), 1)
+        info["clock_split"] = {"camera": cyc[0] / tot, "hit_search": cyc[1] / tot, "shade": cyc[2] / tot,
+                               "accumulate": cyc[3] / tot}
         info["variant"] = stats["dbg_variant"]
         out["stats"] = info
         print(json.dumps(info))

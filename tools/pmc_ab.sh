@@ -1,2 +1,2 @@
 mkdir -p gpurun_out
-PMC_PASSES="waves insts lds" bash profiles/pmc.sh gpurun_out/pmc_v11 --variant 11 --lpp 4
+PMC_PASSES="waves insts lds fetch write" bash profiles/pmc.sh gpurun_out/pmc_v11b
