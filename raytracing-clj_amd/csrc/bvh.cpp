@@ -14,7 +14,7 @@
 //
 // Layout (device, all 16-byte aligned):
 //   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
-//                    slab tests, child refs: >= 0 node, < 0 leaf ~pair (every
+//                    slab tests, relative to the tree centre, child refs: >= 0 node, < 0 leaf ~pair (every
 //                    child is real: small trees repeat a leaf / use a pad leaf)
 //   pairs[n_pairs]   two bodies per leaf: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
 //                    a missing second body has w = +inf: never a candidate)
@@ -206,6 +206,17 @@ int bvh_build(const float* sph, int n, BvhHost* out) {
   }
   root.child[0] = c0;
   root.child[1] = c1;
+  // every node box relative to the centre, in double, rounded outward: the
+  // kernel's slab test is then one fma per bound with a small rounding error
+  for (BvhNode& nd : out->nodes) {
+    float* lo[3] = {nd.minx, nd.miny, nd.minz};
+    float* hi[3] = {nd.maxx, nd.maxy, nd.maxz};
+    for (int k = 0; k < 3; ++k)
+      for (int c = 0; c < 2; ++c) {
+        lo[k][c] = std::nextafter(static_cast<float>(double(lo[k][c]) - out->center[k]), -INFINITY);
+        hi[k][c] = std::nextafter(static_cast<float>(double(hi[k][c]) - out->center[k]), INFINITY);
+      }
+  }
   out->depth = b.max_depth + 1;
   return 0;
 }

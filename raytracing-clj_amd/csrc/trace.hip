@@ -69,6 +69,7 @@ struct alignas(16) KArgs {
   int bvh_off_pairs;     // byte offsets inside the blob
   int bvh_off_pidx;
   int n_big;
+  int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   int spp, sample_begin, max_depth;
   uint32_t key;
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
     __syncthreads();
   }
-  // BVH traversal stack: kBvhStack node indices per lane, [entry][lane] (no bank conflicts)
+  // BVH traversal stack: bvh_stack node refs per lane, [entry][lane] (no bank conflicts)
   unsigned short* s_stack = reinterpret_cast<unsigned short*>(
       reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
 
@@ -349,15 +350,26 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const KNode* nodes = reinterpret_cast<const KNode*>(base);
       const Pair* pairs = reinterpret_cast<const Pair*>(base + a.bvh_off_pairs);
       const int2* pidx = reinterpret_cast<const int2*>(base + a.bvh_off_pidx);
-      const float ecx = ox - a.bvh_c[0], ecy = oy - a.bvh_c[1], ecz = oz - a.bvh_c[2];
       // box tests only cull (conservatively): hardware sqrt / rcp (1 ulp) are
-      // far inside the padding
+      // far inside the padding.  Node boxes are stored relative to the tree
+      // centre c (bvh.cpp), so every slab bound is one fma:
+      // (b - (o' + P)) / u = b * (1/u) - (o' + P) / u with o' = o - c; its
+      // rounding (~1e-7 * D) is far inside the padding too.
+      const float ecx = ox - a.bvh_c[0], ecy = oy - a.bvh_c[1], ecz = oz - a.bvh_c[2];
       const float D = __builtin_amdgcn_sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
       const float P = fmaf(2e-3f, D, 1e-6f);
-      const float rux = __builtin_amdgcn_rcpf(ux), ruy = __builtin_amdgcn_rcpf(uy), ruz = __builtin_amdgcn_rcpf(uz);
+      // |u| >= 1e-24 keeps 1/u finite: with u = 0 an infinite 1/u makes the
+      // fma bounds NaN and -inf, which would collapse the slab (a false miss);
+      // finite, the slab of an origin inside the padded box spans ~+-1e24 and
+      // one outside it lies ~1e24 away (culled) -- the u = 0 answers.
+      const float rux = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(ux), 1e-24f), ux));
+      const float ruy = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uy), 1e-24f), uy));
+      const float ruz = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uz), 1e-24f), uz));
       const f2 ix2 = {rux, rux}, iy2 = {ruy, ruy}, iz2 = {ruz, ruz};
-      const f2 lox = {ox + P, ox + P}, loy = {oy + P, oy + P}, loz = {oz + P, oz + P};
-      const f2 hix = {ox - P, ox - P}, hiy = {oy - P, oy - P}, hiz = {oz - P, oz - P};
+      const float nlx = -(ecx + P) * rux, nly = -(ecy + P) * ruy, nlz = -(ecz + P) * ruz;
+      const float nhx = -(ecx - P) * rux, nhy = -(ecy - P) * ruy, nhz = -(ecz - P) * ruz;
+      const f2 lox = {nlx, nlx}, loy = {nly, nly}, loz = {nlz, nlz};
+      const f2 hix = {nhx, nhx}, hiy = {nhy, nhy}, hiz = {nhz, nhz};
       const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
       const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
       auto leaf = [&](int p) {
@@ -375,9 +387,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // predicate "[tn, tf] meets (tmin, best_t]" (tmin < best_t always; a NaN
       // bound only makes the test pass: conservative)
       auto node_test = [&](const KNode& nd, float& tn0, float& tn1, bool& hit0, bool& hit1) {
-        const f2 t1x = (nd.minx - lox) * ix2, t2x = (nd.maxx - hix) * ix2;
-        const f2 t1y = (nd.miny - loy) * iy2, t2y = (nd.maxy - hiy) * iy2;
-        const f2 t1z = (nd.minz - loz) * iz2, t2z = (nd.maxz - hiz) * iz2;
+        const f2 t1x = fma2(nd.minx, ix2, lox), t2x = fma2(nd.maxx, ix2, hix);
+        const f2 t1y = fma2(nd.miny, iy2, loy), t2y = fma2(nd.maxy, iy2, hiy);
+        const f2 t1z = fma2(nd.minz, iz2, loz), t2z = fma2(nd.maxz, iz2, hiz);
         tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
         const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
         tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
@@ -461,9 +473,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           }
         }
         const KNode nd = nodes[node];
-        const f2 t1x = (nd.minx - lox) * ix2, t2x = (nd.maxx - hix) * ix2;
-        const f2 t1y = (nd.miny - loy) * iy2, t2y = (nd.maxy - hiy) * iy2;
-        const f2 t1z = (nd.minz - loz) * iz2, t2z = (nd.maxz - hiz) * iz2;
+        const f2 t1x = fma2(nd.minx, ix2, lox), t2x = fma2(nd.maxx, ix2, hix);
+        const f2 t1y = fma2(nd.miny, iy2, loy), t2y = fma2(nd.maxy, iy2, hiy);
+        const f2 t1z = fma2(nd.minz, iz2, loz), t2z = fma2(nd.maxz, iz2, hiz);
         const float tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
         const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
         const float tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
@@ -1028,6 +1040,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.bvh_off_pairs = ds->bvh_off_pairs;
   a.bvh_off_pidx = ds->bvh_off_pidx;
   a.n_big = ds->n_big;
+  a.bvh_stack = ds->bvh_depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = ds->bvh_c[k];
   a.bvh_r = ds->bvh_r;
   a.sph = ds->sph;
@@ -1057,7 +1070,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
   int vsel = g_variant;
-  const size_t stack_bytes = static_cast<size_t>(kBvhStack) * 256 * sizeof(unsigned short);
+  const size_t stack_bytes = static_cast<size_t>(ds->bvh_depth + 2) * 256 * sizeof(unsigned short);
   const size_t bvh_lds = static_cast<size_t>(ds->bvh_blob_f4) * 16 + stack_bytes;
   if (vsel == 0) vsel = 11;
   if (vsel >= 11 && vsel <= 15) {

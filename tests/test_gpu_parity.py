@@ -302,3 +302,22 @@ def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
             lib.rt_set_variant(old)
         assert np.array_equal(a, b), (w, h, int((a != b).any(axis=-1).sum()))
         assert st_a["segments"] == st_b["segments"]
+
+
+def test_bvh_axis_aligned_rays(gpu_lib):
+    """Rays with exactly-zero direction components (axis-aligned camera looking
+    down -z at pixel centres on the axes) through the BVH == the scan."""
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import lib
+    sc = scenes.cover(11)
+    # vfov / position chosen so the centre column and row give u_x = 0 / u_y = 0
+    cam = R.camera(65, 37, 60.0, (0.0, 1.0, 12.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), 0.0, 12.0)
+    out = {}
+    for v in (5, 11):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 65, 37, spp=64, seed=3)
+        finally:
+            lib.rt_set_variant(old)
+    assert np.array_equal(out[5], out[11])
