@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4; big-body scan test = 16
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v11"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -106,10 +106,16 @@ def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
             "host": platform.node()}
 
 
-def bvh_counters(ds, cam, p, out, counters, sh):
-    """One untimed launch of the stats build (variant 13) of the same frame:
-    per-segment node visits, leaf-pair tests, exact tests (rt_debug_stats)."""
-    old = lib.rt_set_variant(13)
+# traversal variant -> (its stats build, body pairs per leaf)
+BVH_STATS = {0: (17, 2), 16: (17, 2), 17: (17, 2), 11: (13, 1), 13: (13, 1), 14: (15, 1), 15: (15, 1)}
+
+
+def bvh_counters(ds, cam, p, out, counters, sh, variant):
+    """One untimed launch of the stats build of the same frame and traversal
+    (variant 17 for the default 16, 13 for 11): per-segment node visits,
+    leaf pair tests, exact tests (rt_debug_stats)."""
+    sv, pairs_per_leaf = BVH_STATS[variant]
+    old = lib.rt_set_variant(sv)
     try:
         dbg = (C.c_uint64 * 16)()
         check(lib.rt_debug_stats(dbg))                  # clear
@@ -121,7 +127,8 @@ def bvh_counters(ds, cam, p, out, counters, sh):
         segs = float(counters[0].item())
     finally:
         lib.rt_set_variant(old)
-    return {"nodes": dbg[2] / segs, "leaf_pairs": dbg[3] / segs, "exact_tests": dbg[4] / segs}
+    return {"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs, "exact_tests": dbg[4] / segs,
+            "stats_variant": sv}
 
 
 def pmc_traffic(kernel_substr="trace_kernel"):
@@ -234,7 +241,7 @@ def main():
         local_stats, tot = ls.cpu(), tt.cpu()
     elapsed, kern_max_ms, kern_avg_ms = local_stats.tolist()
     segs_total, samples_total = tot.tolist()
-    bvh = bvh_counters(ds, cam, p, out, counters, sh) if rank == 0 and a.variant in (0, 11, 13) else None
+    bvh = bvh_counters(ds, cam, p, out, counters, sh, a.variant) if rank == 0 and a.variant in BVH_STATS else None
     lib.rt_scene_free(ds)
 
     if rank == 0:
@@ -269,9 +276,10 @@ def main():
                        "width": W, "height": H, "spp_per_gpu": spp, "max_depth": depth, "bodies": len(scene),
                        "parallelism": ("sample-stripe x%d (weak)" % world) if a.scaling == "weak"
                        else ("row-tile 8 x%d (strong)" % world), "variant": a.variant},
-            "roofline": {"bound": "valu", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "roofline": {"bound": "mfma", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": tflops / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "note": f"fp32 VALU (no MFMA: branchy scalar FP); {work}; peak = fp32 vector peak. "
+                         "note": f"compute-bound fp32 on the VALU (branchy per-ray FP work, no GEMM shape: MFMA unused); "
+                                 f"peak = the fp32 dense peak (vector = MFMA for fp32); {work}. "
                                  f"Brute-force-equivalent (SURVEY §8d: 17 x {len(scene)} + 100 per segment): "
                                  f"{bf_tflops:.1f} TF/s. traffic = HBM bytes/launch from {traffic_src} "
                                  f"(FETCH x2 + WRITE)"},
@@ -281,7 +289,7 @@ def main():
             "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
-            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = BVH in LDS, 4 lanes/pixel)" % a.variant,
+            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 4 lanes/pixel)" % a.variant,
             "cpu_baseline": None,
         }
         if a.cpu_baseline == "auto" and world == 1:

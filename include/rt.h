@@ -168,9 +168,11 @@ int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
 
 /* Kernel variant selector for A/B measurement (all variants give identical
- * bits): 0 = default (11); 11 = BVH traversal with nodes and leaf bodies in
- * LDS, 12 = the same reading the tree from global memory (used when the
- * tree does not fit LDS), 13 = 11 with statistics; 1 = sphere table in LDS, one body per step;
+ * bits): 0 = default (16); 16 = BVH traversal, 4 bodies per leaf, nodes and
+ * leaf bodies in LDS, 17 = 16 with statistics; 11 = the same with 2 bodies
+ * per leaf, 12 = 11 reading the tree from global memory (used when a tree
+ * does not fit LDS), 13 = 11 with statistics, 14 / 15 = 11 with a
+ * speculative while-while traversal (+ statistics); 1 = sphere table in LDS, one body per step;
  * 2 = table through the scalar cache, one body per step; 4 = LDS table,
  * bodies in groups of 4 with the next group prefetched; 5 = scalar-cache
  * table, grouped; 8 / 9 = 4 / 5 with two bodies per packed-fp32

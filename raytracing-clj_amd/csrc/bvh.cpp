@@ -16,8 +16,9 @@
 //   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
 //                    slab tests, relative to the tree centre, child refs: >= 0 node, < 0 leaf ~pair (every
 //                    child is real: small trees repeat a leaf / use a pad leaf)
-//   pairs[n_pairs]   two bodies per leaf: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
-//                    a missing second body has w = +inf: never a candidate)
+//   pairs[n_pairs]   two bodies per pair: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
+//                    a missing body has w = +inf: never a candidate); a leaf
+//                    is 1 pair (leaf_size 2) or 2 consecutive pairs (4)
 //   pidx[n_pairs]    original indices of the two bodies (-1 for the pad)
 #include "bvh.h"
 
@@ -58,30 +59,36 @@ struct Builder {
   BvhHost* out;
   int max_depth = 0;
 
+  int leaf_size = 2;       // bodies per leaf: 2 (one pair) or 4 (two pairs)
+
   int leaf(int lo, int cnt, Box* box) {
     const int p = static_cast<int>(out->pidx.size() / 2);
-    float pair[8] = {0, 0, 0, 0, 0, 0, INFINITY, INFINITY};
-    int idx[2] = {-1, -1};
-    for (int j = 0; j < cnt; ++j) {
-      const float* s = sph + 4 * prim[lo + j];
-      pair[0 + j] = s[0];
-      pair[2 + j] = s[1];
-      pair[4 + j] = s[2];
-      pair[6 + j] = -(s[3] * s[3]);
-      idx[j] = prim[lo + j];
-      box->add(body_box(s));
+    for (int q = 0; q < leaf_size / 2; ++q) {
+      float pair[8] = {0, 0, 0, 0, 0, 0, INFINITY, INFINITY};
+      int idx[2] = {-1, -1};
+      for (int j = 0; j < 2; ++j) {
+        const int k = 2 * q + j;
+        if (k >= cnt) break;
+        const float* s = sph + 4 * prim[lo + k];
+        pair[0 + j] = s[0];
+        pair[2 + j] = s[1];
+        pair[4 + j] = s[2];
+        pair[6 + j] = -(s[3] * s[3]);
+        idx[j] = prim[lo + k];
+        box->add(body_box(s));
+      }
+      out->pairs.insert(out->pairs.end(), pair, pair + 8);
+      out->pidx.push_back(idx[0]);
+      out->pidx.push_back(idx[1]);
     }
-    out->pairs.insert(out->pairs.end(), pair, pair + 8);
-    out->pidx.push_back(idx[0]);
-    out->pidx.push_back(idx[1]);
-    return ~p;   // < 0: leaf
+    return ~p;   // < 0: leaf (its first pair)
   }
 
   // returns a child ref (node index >= 0, or ~leaf) and its box
   int build(int lo, int hi, int depth, Box* box) {
     max_depth = std::max(max_depth, depth);
     const int cnt = hi - lo;
-    if (cnt <= 2) return leaf(lo, cnt, box);
+    if (cnt <= leaf_size) return leaf(lo, cnt, box);
     Box cb;  // centroid bounds
     for (int i = lo; i < hi; ++i) {
       const float* s = sph + 4 * prim[i];
@@ -93,9 +100,11 @@ struct Builder {
     int axis = 0;
     for (int k = 1; k < 3; ++k)
       if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
-    // median split on an even boundary: balanced depth, full leaf pairs
-    int mid = lo + ((cnt / 2 + 1) & ~1);
-    if (mid >= hi) mid = lo + 2;
+    // median split on a leaf-size boundary: balanced depth, full leaves
+    const int L = leaf_size;
+    int mid = lo + ((cnt / 2 + L / 2) / L) * L;
+    if (mid <= lo) mid = lo + L;
+    if (mid >= hi) mid = hi - 1;
     std::nth_element(prim.begin() + lo, prim.begin() + mid, prim.begin() + hi, [&](int a, int b) {
       const float ca = sph[4 * a + axis], cb_ = sph[4 * b + axis];
       return ca < cb_ || (ca == cb_ && a < b);
@@ -125,8 +134,10 @@ struct Builder {
 
 }  // namespace
 
-int bvh_build(const float* sph, int n, BvhHost* out) {
+int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size) {
   *out = BvhHost{};
+  if (leaf_size != 2 && leaf_size != 4) leaf_size = 2;
+  out->leaf_size = leaf_size;
   // big bodies: scanned first, outside the tree
   std::vector<float> radii;
   for (int i = 0; i < n; ++i) radii.push_back(std::fabs(sph[4 * i + 3]));
@@ -137,6 +148,7 @@ int bvh_build(const float* sph, int n, BvhHost* out) {
     med = tmp[n / 2];
   }
   Builder b{sph, {}, out};
+  b.leaf_size = leaf_size;
   for (int i = 0; i < n; ++i) {
     const bool finite = std::isfinite(sph[4 * i]) && std::isfinite(sph[4 * i + 1]) &&
                         std::isfinite(sph[4 * i + 2]) && std::isfinite(sph[4 * i + 3]);
@@ -171,9 +183,12 @@ int bvh_build(const float* sph, int n, BvhHost* out) {
     for (int k = 0; k < 3; ++k) b0.lo[k] = b0.hi[k] = 0.0f;
     b1 = b0;
   } else {
-    const int mid = cnt <= 2 ? cnt : ((cnt / 2 + 1) & ~1);
+    const int L = leaf_size;
+    int mid = ((cnt / 2 + L / 2) / L) * L;
+    if (mid <= 0) mid = L;
+    if (mid >= cnt) mid = cnt - 1;
     // split the root by the same rule as build() (axis from centroid bounds)
-    if (cnt <= 2) {
+    if (cnt <= L) {
       c0 = c1 = b.leaf(0, cnt, &b0);   // the same leaf twice: a repeat test never wins a tie
       b1 = b0;
     } else {

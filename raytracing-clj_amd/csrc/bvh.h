@@ -22,9 +22,10 @@ struct BvhHost {
   float center[3] = {0, 0, 0};
   float radius = 0.0f;        // bounding sphere of the tree's bodies
   int depth = 0;              // levels of nodes on the longest root-leaf path
+  int leaf_size = 2;          // bodies per leaf (2: one pair, 4: two pairs)
 };
 
-int bvh_build(const float* sphere, int n, BvhHost* out);
+int bvh_build(const float* sphere, int n, BvhHost* out, int leaf_size = 2);
 
 // traversal stack entries per lane (node indices); trees are median-split, so
 // depth <= ceil(log2(n/2)) + 1 (13 for 8192 bodies)

@@ -125,7 +125,9 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
-enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4, SCAN_BVHQ = 5 };
+// the traversal variants (BVHQ: ordered traversal of the 4-body-leaf tree)
+constexpr bool is_bvh_scan(int scan) { return scan == SCAN_BVH || scan == SCAN_BVHWW || scan == SCAN_BVHQ; }
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVHWW) {
+  if constexpr (is_bvh_scan(SCAN)) {
     if constexpr (SRC == SRC_LDS) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
       __syncthreads();
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // h < 0 && c >= 0: both roots <= 0 (exact in fp: sqrt(RN(h*h)) = |h|)
         if ((disc >= 0.0f) & ((h >= 0.0f) | (c < 0.0f))) consider(h, disc, s);
       }
-    } else if constexpr (SCAN == SCAN_BVH || SCAN == SCAN_BVHWW) {
+    } else if constexpr (is_bvh_scan(SCAN)) {
       // Closest hit through the BVH (bvh.cpp), bit-identical to the scan:
       //  * each body is tested by the scan's fp32 op sequence and accepted if
       //    t is smaller, or equal with a lower index (= the scan's first-wins);
@@ -324,15 +326,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       //    tools/pad_bound.cpp, 3x margin), so a body the scan would accept
       //    always lies in every box on its path; a box is skipped only if its
       //    padded interval misses (tmin, best_t].
+      // branch-free acceptance (bitwise predicates: no exec-mask blocks)
       auto consider_tie = [&](float h, float disc, int s) {
         if constexpr (STATS) ++st_blk_lanes;
         const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
-        float t = h - sq;
-        if (!(t > tmin)) t = h + sq;
-        if (t > tmin && (t < best_t || (t == best_t && s < best))) {
-          best_t = t;
-          best = s;
-        }
+        const float tn = h - sq;
+        const float t = tn > tmin ? tn : h + sq;
+        const bool acc = (t > tmin) & ((t < best_t) | ((t == best_t) & (s < best)));
+        best_t = acc ? t : best_t;
+        best = acc ? s : best;
       };
       // 1) big bodies (kept out of the tree), ascending index
       for (int i = 0; i < a.n_big; ++i) {
@@ -372,16 +374,46 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const f2 hix = {nhx, nhx}, hiy = {nhy, nhy}, hiz = {nhz, nhz};
       const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
       const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
+      // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
+      // size 4), tested packed; the acceptance is order-independent
       auto leaf = [&](int p) {
         if constexpr (STATS) ++st_blk;
-        const Pair g = pairs[p];
-        const int2 id = pidx[p];
-        const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
-        const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
-        const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
-        const f2 disc = fma2(h, h, -c);
-        if (fminf(disc.x, fmaxf(h.x, -c.x)) >= 0.0f) consider_tie(h.x, disc.x, id.x);
-        if (fminf(disc.y, fmaxf(h.y, -c.y)) >= 0.0f) consider_tie(h.y, disc.y, id.y);
+        constexpr int NP = SCAN == SCAN_BVHQ ? 2 : 1;
+        float hh[2 * NP], dd[2 * NP];
+        int ii[2 * NP];
+        unsigned m = 0;   // candidate bodies of the leaf
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const Pair g = pairs[p + q];
+          const int2 id = pidx[p + q];
+          const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
+          const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
+          const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
+          const f2 disc = fma2(h, h, -c);
+          hh[2 * q] = h.x;
+          hh[2 * q + 1] = h.y;
+          dd[2 * q] = disc.x;
+          dd[2 * q + 1] = disc.y;
+          ii[2 * q] = id.x;
+          ii[2 * q + 1] = id.y;
+          m |= static_cast<unsigned>(fminf(disc.x, fmaxf(h.x, -c.x)) >= 0.0f) << (2 * q);
+          m |= static_cast<unsigned>(fminf(disc.y, fmaxf(h.y, -c.y)) >= 0.0f) << (2 * q + 1);
+        }
+        // one pass of the exact test per candidate: the wave runs it as often
+        // as its lane with the most candidates needs (not once per body)
+        while (m) {
+          const unsigned k = __builtin_ctz(m);
+          m &= m - 1;
+          float h = hh[0], d = dd[0];
+          int s = ii[0];
+#pragma unroll
+          for (int j = 1; j < 2 * NP; ++j) {
+            h = k == static_cast<unsigned>(j) ? hh[j] : h;
+            d = k == static_cast<unsigned>(j) ? dd[j] : d;
+            s = k == static_cast<unsigned>(j) ? ii[j] : s;
+          }
+          consider_tie(h, d, s);
+        }
       };
       // slab test of both children of node nd: entry/exit t and the cull
       // predicate "[tn, tf] meets (tmin, best_t]" (tmin < best_t always; a NaN
@@ -484,14 +516,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // makes the test pass: conservative)
         bool hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
         bool hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
-        if (hit0 && nd.c0 < 0) {
-          leaf(~nd.c0);
-          hit0 = false;
+        // leaf children are tested now; a lane's first leaf shares one pass
+        // with every other lane's first leaf, whichever child it is
+        const bool l0 = hit0 & (nd.c0 < 0), l1 = hit1 & (nd.c1 < 0);
+        if (l0 | l1) {
+          leaf(l0 ? ~nd.c0 : ~nd.c1);
+          if (l0 & l1) leaf(~nd.c1);
         }
-        if (hit1 && nd.c1 < 0) {
-          leaf(~nd.c1);
-          hit1 = false;
-        }
+        hit0 = hit0 & !l0;
+        hit1 = hit1 & !l1;
         if (hit0 && hit1) {
           const bool sw = tn1 < tn0;
           s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? nd.c0 : nd.c1);
@@ -580,7 +613,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         g3 = n3;
       }
     }
-    if constexpr (STATS && SCAN != SCAN_BVH && SCAN != SCAN_BVHWW) {
+    if constexpr (STATS && !is_bvh_scan(SCAN)) {
       const uint64_t ex = __builtin_amdgcn_read_exec();
       if (lane == __ffsll(static_cast<long long>(ex)) - 1) st_sph += static_cast<uint64_t>(n);
     }
@@ -813,8 +846,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 //   8 LDS table, packed pairs      9 scalar, packed pairs   10 = 9 + stats
 //  11 BVH in LDS                  12 BVH in global memory   13 = 11 + stats
 //  14 BVH in LDS, speculative while-while traversal          15 = 14 + stats
+//  16 BVH in LDS, 4-body leaves (two pairs)                  17 = 16 + stats
 //     (BVH variants fall back to 5 when the tree does not fit / is too deep)
-//   0 = default (11)
+//   0 = default (16)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
 // 0 = automatic (enough waves to keep the chip full to the end).
 struct Variant {
@@ -822,9 +856,10 @@ struct Variant {
   bool lds;
   bool stats;
 };
+constexpr int kVariants = 18;
 #define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
 static const Variant& variant_table(int v) {
-  static const Variant t[16] = {
+  static const Variant t[kVariants] = {
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
         RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
@@ -854,8 +889,12 @@ static const Variant& variant_table(int v) {
         RT_K(SRC_LDS, SCAN_BVHWW, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHWW, 1, true), RT_K(SRC_LDS, SCAN_BVHWW, 2, true),
         RT_K(SRC_LDS, SCAN_BVHWW, 4, true)}, true, true},
+      {{RT_K(SRC_LDS, SCAN_BVHQ, 1, false), RT_K(SRC_LDS, SCAN_BVHQ, 2, false),
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, false)}, true, false},
+      {{RT_K(SRC_LDS, SCAN_BVHQ, 1, true), RT_K(SRC_LDS, SCAN_BVHQ, 2, true),
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, true)}, true, true},
   };
-  return t[(v >= 0 && v < 16) ? v : 0];
+  return t[(v >= 0 && v < kVariants) ? v : 0];
 }
 #undef RT_K
 static int g_lpp = 0;  // 0 = automatic
@@ -880,17 +919,22 @@ static unsigned long long* g_dbgw = nullptr;  // device u64[4 * 65536] wave time
 
 using namespace rtclj;
 
+// one BVH on the device: blob = nodes | pairs | pidx, and the big-body list
+struct DTree {
+  float4* blob;
+  int* big;
+  int blob_f4, off_pairs, off_pidx, n_big, depth;
+  float c[3], r;
+};
+
 struct rt_dscene {
   int device;
   int n;
   int n_pad;
   float4* geo;
   float4* geo2;   // n_pad/2 Pairs (= n_pad float4)
-  // BVH (bvh.cpp): device blob nodes | pairs | pidx and the big-body list
-  float4* bvh_blob;
-  int* bvh_big;
-  int bvh_blob_f4, bvh_off_pairs, bvh_off_pidx, n_big, bvh_depth;
-  float bvh_c[3], bvh_r;
+  // BVHs (bvh.cpp): tree[0] 2-body leaves, tree[1] 4-body leaves
+  DTree tree[2];
   float4* sph;
   float4* mat;
   int* kind;
@@ -908,7 +952,7 @@ static int hip_fail(hipError_t e, const char* what) {
 
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
-  if (v >= 0 && v <= 15) g_variant = v;
+  if (v >= 0 && v < kVariants) g_variant = v;
   return old;
 }
 
@@ -964,34 +1008,37 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     o[0] = b0.x; o[1] = b1.x; o[2] = b0.y; o[3] = b1.y;
     o[4] = b0.z; o[5] = b1.z; o[6] = b0.w; o[7] = b1.w;
   }
-  // BVH over the bodies (the traversal variants): blob = nodes | pairs | pidx
-  BvhHost bvh;
-  bvh_build(s->sphere, n, &bvh);
-  const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
-  const size_t pb = bvh.pairs.size() * sizeof(float);
-  const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;
-  std::vector<char> blob(nb + pb + ib, 0);
-  std::memcpy(blob.data(), bvh.nodes.data(), nb);
-  std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
-  std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
-  std::vector<int> big = bvh.big;
-  if (big.empty()) big.push_back(0);
   rt_dscene* d = new rt_dscene{};
   d->device = device;
   d->n = n;
   d->n_pad = n_pad;
-  d->bvh_blob_f4 = static_cast<int>(blob.size() / 16);
-  d->bvh_off_pairs = static_cast<int>(nb);
-  d->bvh_off_pidx = static_cast<int>(nb + pb);
-  d->n_big = static_cast<int>(bvh.big.size());
-  d->bvh_depth = bvh.depth;
-  for (int k = 0; k < 3; ++k) d->bvh_c[k] = bvh.center[k];
-  d->bvh_r = bvh.radius;
   hipError_t e = hipMalloc(&d->geo, n_pad * sizeof(float4));
-  if (e == hipSuccess) e = hipMalloc(&d->bvh_blob, blob.size());
-  if (e == hipSuccess) e = hipMemcpy(d->bvh_blob, blob.data(), blob.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&d->bvh_big, big.size() * sizeof(int));
-  if (e == hipSuccess) e = hipMemcpy(d->bvh_big, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice);
+  // BVHs over the bodies (the traversal variants): blob = nodes | pairs | pidx
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    BvhHost bvh;
+    bvh_build(s->sphere, n, &bvh, k == 0 ? 2 : 4);
+    const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
+    const size_t pb = bvh.pairs.size() * sizeof(float);
+    const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;
+    std::vector<char> blob(nb + pb + ib, 0);
+    std::memcpy(blob.data(), bvh.nodes.data(), nb);
+    std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
+    std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
+    std::vector<int> big = bvh.big;
+    if (big.empty()) big.push_back(0);
+    DTree& t = d->tree[k];
+    t.blob_f4 = static_cast<int>(blob.size() / 16);
+    t.off_pairs = static_cast<int>(nb);
+    t.off_pidx = static_cast<int>(nb + pb);
+    t.n_big = static_cast<int>(bvh.big.size());
+    t.depth = bvh.depth;
+    for (int j = 0; j < 3; ++j) t.c[j] = bvh.center[j];
+    t.r = bvh.radius;
+    e = hipMalloc(&t.blob, blob.size());
+    if (e == hipSuccess) e = hipMemcpy(t.blob, blob.data(), blob.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&t.big, big.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(t.big, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMalloc(&d->geo2, n_pad * sizeof(float4));
   if (e == hipSuccess) e = hipMemcpy(d->geo2, geo2.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&d->sph, cnt * sizeof(float4));
@@ -1014,8 +1061,10 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   (void)hipSetDevice(d->device);
   if (d->geo) (void)hipFree(d->geo);
   if (d->geo2) (void)hipFree(d->geo2);
-  if (d->bvh_blob) (void)hipFree(d->bvh_blob);
-  if (d->bvh_big) (void)hipFree(d->bvh_big);
+  for (const DTree& t : d->tree) {
+    if (t.blob) (void)hipFree(t.blob);
+    if (t.big) (void)hipFree(t.big);
+  }
   if (d->sph) (void)hipFree(d->sph);
   if (d->mat) (void)hipFree(d->mat);
   if (d->kind) (void)hipFree(d->kind);
@@ -1034,15 +1083,6 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   KArgs a{};
   a.geo = ds->geo;
   a.geo2 = reinterpret_cast<const Pair*>(ds->geo2);
-  a.bvh_blob = ds->bvh_blob;
-  a.bvh_big = ds->bvh_big;
-  a.bvh_blob_f4 = ds->bvh_blob_f4;
-  a.bvh_off_pairs = ds->bvh_off_pairs;
-  a.bvh_off_pidx = ds->bvh_off_pidx;
-  a.n_big = ds->n_big;
-  a.bvh_stack = ds->bvh_depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
-  for (int k = 0; k < 3; ++k) a.bvh_c[k] = ds->bvh_c[k];
-  a.bvh_r = ds->bvh_r;
   a.sph = ds->sph;
   a.mat = ds->mat;
   a.kind = ds->kind;
@@ -1070,15 +1110,29 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
   int vsel = g_variant;
-  const size_t stack_bytes = static_cast<size_t>(ds->bvh_depth + 2) * 256 * sizeof(unsigned short);
-  const size_t bvh_lds = static_cast<size_t>(ds->bvh_blob_f4) * 16 + stack_bytes;
-  if (vsel == 0) vsel = 11;
-  if (vsel >= 11 && vsel <= 15) {
-    if (ds->bvh_depth + 2 > kBvhStack) vsel = 5;               // tree too deep for the stack
-    else if (vsel != 12 && bvh_lds > 96 * 1024) vsel = 12;      // tree too big for LDS
+  if (vsel == 0) vsel = 16;
+  auto stack_of = [](const DTree& t) { return static_cast<size_t>(t.depth + 2) * 256 * sizeof(unsigned short); };
+  auto lds_of = [&](const DTree& t) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t); };
+  if (vsel >= 11) {
+    const DTree& t = ds->tree[vsel >= 16 ? 1 : 0];
+    if (t.depth + 2 > kBvhStack) vsel = 5;                      // tree too deep for the stack
+    else if (vsel != 12 && lds_of(t) > 96 * 1024) vsel = 12;    // tree too big for LDS: 2-body leaves, global
   }
+  const DTree& tr = ds->tree[vsel >= 16 ? 1 : 0];
+  if (vsel == 12 && tr.depth + 2 > kBvhStack) vsel = 5;
+  const size_t stack_bytes = stack_of(tr);
+  const size_t bvh_lds = lds_of(tr);
   const Variant& v = variant_table(vsel);
-  const bool is_bvh = vsel >= 11 && vsel <= 15;
+  const bool is_bvh = vsel >= 11;
+  a.bvh_blob = tr.blob;
+  a.bvh_big = tr.big;
+  a.bvh_blob_f4 = tr.blob_f4;
+  a.bvh_off_pairs = tr.off_pairs;
+  a.bvh_off_pidx = tr.off_pidx;
+  a.n_big = tr.n_big;
+  a.bvh_stack = tr.depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
+  for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
+  a.bvh_r = tr.r;
   const int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr);
   const int tw = lpp == 4 ? 4 : 8, th = lpp == 1 ? 8 : 4;   // wave tile (trace_kernel)
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));

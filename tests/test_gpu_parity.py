@@ -161,7 +161,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("lpp", [1, 2, 4])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
@@ -176,7 +176,7 @@ def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     try:
         st = {}
         g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7, 10, 13, 15):
+        if variant in (3, 6, 7, 10, 13, 15, 17):
             import ctypes as C
             d = (C.c_uint64 * 16)()
             lib.rt_debug_stats(d)
@@ -280,7 +280,7 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("variant", [11, 12, 14])
+@pytest.mark.parametrize("variant", [11, 12, 14, 16])
 def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
@@ -314,10 +314,67 @@ def test_bvh_axis_aligned_rays(gpu_lib):
     # vfov / position chosen so the centre column and row give u_x = 0 / u_y = 0
     cam = R.camera(65, 37, 60.0, (0.0, 1.0, 12.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), 0.0, 12.0)
     out = {}
-    for v in (5, 11):
+    for v in (5, 11, 16):
         old = lib.rt_set_variant(v)
         try:
             out[v] = R.render(sc, cam, 65, 37, spp=64, seed=3)
         finally:
             lib.rt_set_variant(old)
     assert np.array_equal(out[5], out[11])
+    assert np.array_equal(out[5], out[16])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 6, 7, 9, 13, 33])
+def test_bvh_small_scenes(gpu_lib, n):
+    """Small and ragged body counts (a leaf-only tree, a repeated leaf, pad
+    bodies in a 2- or 4-body leaf) through both trees == the scan."""
+    from rtclj import raytracing as R
+    from rtclj._lib import lib
+    rng = np.random.default_rng(n)
+    sph = np.zeros((n, 4), np.float32)
+    sph[:, 0] = rng.uniform(-3, 3, n)
+    sph[:, 1] = rng.uniform(0, 2, n)
+    sph[:, 2] = rng.uniform(-6, -1, n)
+    sph[:, 3] = rng.uniform(0.2, 0.9, n)
+    kind = rng.integers(0, 3, n).astype(np.int32)
+    mat = np.column_stack([rng.uniform(0, 1, (n, 3)), np.where(kind == 2, 1.5, 0.3)]).astype(np.float32)
+    sc = R.Scene(sph, kind, mat)
+    cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
+    out = {}
+    for v in (5, 11, 16):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5)
+        finally:
+            lib.rt_set_variant(old)
+    assert np.array_equal(out[5], out[11])
+    assert np.array_equal(out[5], out[16])
+    ref, _, _ = _mirror(sc, cam, 48, 27, 8, 20, seed=5)
+    assert np.array_equal(out[5], ref)
+
+
+@pytest.mark.parametrize("variant", [11, 16])
+def test_bvh_large_scene_falls_back(gpu_lib, variant):
+    """8192 bodies: the trees exceed the LDS budget, the launch falls back to
+    the global-memory traversal of the 2-body tree: same bits as the scan."""
+    from rtclj import raytracing as R
+    from rtclj._lib import lib, RT_MAX_SPHERES
+    rng = np.random.default_rng(1)
+    n = RT_MAX_SPHERES
+    sph = np.zeros((n, 4), np.float32)
+    sph[:, 0] = rng.uniform(-40, 40, n)
+    sph[:, 1] = rng.uniform(-1, 3, n)
+    sph[:, 2] = rng.uniform(-60, -5, n)
+    sph[:, 3] = rng.uniform(0.05, 0.3, n)
+    kind = rng.integers(0, 3, n).astype(np.int32)
+    mat = np.column_stack([rng.uniform(0, 1, (n, 3)), np.where(kind == 2, 1.5, 0.3)]).astype(np.float32)
+    sc = R.Scene(sph, kind, mat)
+    cam = R.camera(96, 54, 40.0, (0, 1, 3), (0, 1, -10), (0, 1, 0), 0.0, 10.0)
+    out = {}
+    for v in (5, variant):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 96, 54, spp=4, max_depth=10, seed=2)
+        finally:
+            lib.rt_set_variant(old)
+    assert np.array_equal(out[5], out[variant])
