@@ -14,8 +14,11 @@
 //
 // Layout (device, all 16-byte aligned):
 //   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
-//                    slab tests, relative to the tree centre, child refs: >= 0 node, < 0 leaf ~pair (every
-//                    child is real: small trees repeat a leaf / use a pad leaf)
+//                    slab tests, per axis (min, max, min) so a ray reads its
+//                    (near, far) planes without ordering them, relative to
+//                    the tree centre; child refs: >= 0 node, < 0 leaf ~pair
+//                    (every child is real: small trees repeat a leaf / use a
+//                    pad leaf)
 //   pairs[n_pairs]   two bodies per pair: x0 x1 y0 y1 z0 z1 w0 w1 (w = -r^2;
 //                    a missing body has w = +inf: never a candidate); a leaf
 //                    is 1 pair (leaf_size 2) or 2 consecutive pairs (4)
@@ -51,6 +54,16 @@ Box body_box(const float* s) {
     b.hi[k] = std::nextafter(s[k] + r, INFINITY);
   }
   return b;
+}
+
+// child c's box into node n: per axis (min, max, min) pairs (bvh.h)
+void set_box(BvhNode& n, int c, const Box& b) {
+  float* ax[3] = {n.x, n.y, n.z};
+  for (int k = 0; k < 3; ++k) {
+    ax[k][c] = b.lo[k];
+    ax[k][2 + c] = b.hi[k];
+    ax[k][4 + c] = b.lo[k];
+  }
 }
 
 struct Builder {
@@ -115,15 +128,8 @@ struct Builder {
     const int c0 = build(lo, mid, depth + 1, &b0);
     const int c1 = build(mid, hi, depth + 1, &b1);
     BvhNode& n = out->nodes[me];
-    const Box* bx[2] = {&b0, &b1};
-    for (int c = 0; c < 2; ++c) {
-      n.minx[c] = bx[c]->lo[0];
-      n.miny[c] = bx[c]->lo[1];
-      n.minz[c] = bx[c]->lo[2];
-      n.maxx[c] = bx[c]->hi[0];
-      n.maxy[c] = bx[c]->hi[1];
-      n.maxz[c] = bx[c]->hi[2];
-    }
+    set_box(n, 0, b0);
+    set_box(n, 1, b1);
     n.child[0] = c0;
     n.child[1] = c1;
     box->add(b0);
@@ -210,26 +216,19 @@ int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size) {
     }
   }
   BvhNode& root = out->nodes[0];
-  const Box* bx[2] = {&b0, &b1};
-  for (int c = 0; c < 2; ++c) {
-    root.minx[c] = bx[c]->lo[0];
-    root.miny[c] = bx[c]->lo[1];
-    root.minz[c] = bx[c]->lo[2];
-    root.maxx[c] = bx[c]->hi[0];
-    root.maxy[c] = bx[c]->hi[1];
-    root.maxz[c] = bx[c]->hi[2];
-  }
+  set_box(root, 0, b0);
+  set_box(root, 1, b1);
   root.child[0] = c0;
   root.child[1] = c1;
   // every node box relative to the centre, in double, rounded outward: the
   // kernel's slab test is then one fma per bound with a small rounding error
   for (BvhNode& nd : out->nodes) {
-    float* lo[3] = {nd.minx, nd.miny, nd.minz};
-    float* hi[3] = {nd.maxx, nd.maxy, nd.maxz};
+    float* ax[3] = {nd.x, nd.y, nd.z};
     for (int k = 0; k < 3; ++k)
       for (int c = 0; c < 2; ++c) {
-        lo[k][c] = std::nextafter(static_cast<float>(double(lo[k][c]) - out->center[k]), -INFINITY);
-        hi[k][c] = std::nextafter(static_cast<float>(double(hi[k][c]) - out->center[k]), INFINITY);
+        ax[k][c] = std::nextafter(static_cast<float>(double(ax[k][c]) - out->center[k]), -INFINITY);
+        ax[k][2 + c] = std::nextafter(static_cast<float>(double(ax[k][2 + c]) - out->center[k]), INFINITY);
+        ax[k][4 + c] = ax[k][c];
       }
   }
   out->depth = b.max_depth + 1;

@@ -5,14 +5,15 @@
 
 namespace rtclj {
 
-// 64 bytes: two child boxes in (child0, child1) float pairs + child refs
+// 80 bytes: the two child boxes, per axis as the (child0, child1) float
+// pairs (min, max, min), so a ray reads its (near, far) planes of an axis as
+// two consecutive pairs -- at offset 0 (1/u >= 0) or 8 (1/u < 0) -- and needs
+// no min/max to order them; then the child refs
 struct alignas(16) BvhNode {
-  float minx[2], miny[2], minz[2];
-  float maxx[2], maxy[2], maxz[2];
+  float x[6], y[6], z[6];
   int child[2];   // >= 0: node, < 0: ~leaf pair index
-  int pad[2];
 };
-static_assert(sizeof(BvhNode) == 64, "BvhNode layout");
+static_assert(sizeof(BvhNode) == 80, "BvhNode layout");
 
 struct BvhHost {
   std::vector<BvhNode> nodes;

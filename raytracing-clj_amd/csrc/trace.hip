@@ -136,11 +136,14 @@ struct alignas(16) Pair {
 };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// BVH node as the kernel reads it (= rtclj::BvhNode, bvh.h)
+// BVH node as the kernel reads it (= rtclj::BvhNode, bvh.h): per axis the
+// (child0, child1) pairs (min, max, min); a ray's (near, far) planes are the
+// pairs at index s, s + 1 with s = 1 if 1/u < 0, else 0
 struct alignas(16) KNode {
-  f2 minx, miny, minz, maxx, maxy, maxz;   // (child0, child1)
-  int c0, c1, pad0, pad1;
+  f2 x[3], y[3], z[3];
+  int c0, c1;
 };
+static_assert(sizeof(KNode) == 80, "KNode layout");
 
 // Sample stripes (arithmetic contract): a pixel's spp samples are split into
 // P = min(4, spp) contiguous stripes (stripe s: samples [s*q + min(s,r),
@@ -368,10 +371,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float ruy = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uy), 1e-24f), uy));
       const float ruz = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uz), 1e-24f), uz));
       const f2 ix2 = {rux, rux}, iy2 = {ruy, ruy}, iz2 = {ruz, ruz};
+      // the min plane's bound b*(1/u) - (o' + P)/u, the max plane's
+      // b*(1/u) - (o' - P)/u; by the sign of 1/u one is the near plane
       const float nlx = -(ecx + P) * rux, nly = -(ecy + P) * ruy, nlz = -(ecz + P) * ruz;
       const float nhx = -(ecx - P) * rux, nhy = -(ecy - P) * ruy, nhz = -(ecz - P) * ruz;
-      const f2 lox = {nlx, nlx}, loy = {nly, nly}, loz = {nlz, nlz};
-      const f2 hix = {nhx, nhx}, hiy = {nhy, nhy}, hiz = {nhz, nhz};
+      const bool sx = rux < 0.0f, sy = ruy < 0.0f, sz = ruz < 0.0f;
+      const f2 nearx = {sx ? nhx : nlx, sx ? nhx : nlx}, farx = {sx ? nlx : nhx, sx ? nlx : nhx};
+      const f2 neary = {sy ? nhy : nly, sy ? nhy : nly}, fary = {sy ? nly : nhy, sy ? nly : nhy};
+      const f2 nearz = {sz ? nhz : nlz, sz ? nhz : nlz}, farz = {sz ? nlz : nhz, sz ? nlz : nhz};
+      // byte offsets of the (near, far) pairs of each axis inside a node
+      const int offx = sx ? 8 : 0, offy = 24 + (sy ? 8 : 0), offz = 48 + (sz ? 8 : 0);
       const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
       const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
       // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
@@ -418,16 +427,25 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // slab test of both children of node nd: entry/exit t and the cull
       // predicate "[tn, tf] meets (tmin, best_t]" (tmin < best_t always; a NaN
       // bound only makes the test pass: conservative)
-      auto node_test = [&](const KNode& nd, float& tn0, float& tn1, bool& hit0, bool& hit1) {
-        const f2 t1x = fma2(nd.minx, ix2, lox), t2x = fma2(nd.maxx, ix2, hix);
-        const f2 t1y = fma2(nd.miny, iy2, loy), t2y = fma2(nd.maxy, iy2, hiy);
-        const f2 t1z = fma2(nd.minz, iz2, loz), t2z = fma2(nd.maxz, iz2, hiz);
-        tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
-        const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
-        tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
-        const float tf1 = fminf(fminf(fmaxf(t1x.y, t2x.y), fmaxf(t1y.y, t2y.y)), fmaxf(t1z.y, t2z.y));
+      // (the near plane's t is the min of the two planes' t, bit for bit: the
+      // same fma on the same operands -- no min/max orders them)
+      auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
+        const char* nb = reinterpret_cast<const char*>(nodes + node);
+        const f2* ax = reinterpret_cast<const f2*>(nb + offx);
+        const f2* ay = reinterpret_cast<const f2*>(nb + offy);
+        const f2* az = reinterpret_cast<const f2*>(nb + offz);
+        const int2 ch = *reinterpret_cast<const int2*>(nb + 72);
+        const f2 tnx = fma2(ax[0], ix2, nearx), tfx = fma2(ax[1], ix2, farx);
+        const f2 tny = fma2(ay[0], iy2, neary), tfy = fma2(ay[1], iy2, fary);
+        const f2 tnz = fma2(az[0], iz2, nearz), tfz = fma2(az[1], iz2, farz);
+        tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
+        tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
+        const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
+        const float tf1 = fminf(fminf(tfx.y, tfy.y), tfz.y);
         hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
         hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
+        c0 = ch.x;
+        c1 = ch.y;
       };
       if constexpr (SCAN == SCAN_BVHWW) {
         // speculative while-while (Aila & Laine 2009): a node phase in which
@@ -448,12 +466,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
                 st_trav_lanes += __popcll(ex);
               }
             }
-            const KNode nd = nodes[node];
             float tn0, tn1;
             bool hit0, hit1;
-            node_test(nd, tn0, tn1, hit0, hit1);
+            int c0, c1;
+            node_test(node, tn0, tn1, hit0, hit1, c0, c1);
             const bool sw = tn1 < tn0;   // near child first
-            const int cn = sw ? nd.c1 : nd.c0, cf = sw ? nd.c0 : nd.c1;
+            const int cn = sw ? c1 : c0, cf = sw ? c0 : c1;
             const bool hn = sw ? hit1 : hit0, hf = sw ? hit0 : hit1;
             int next = -1;
             if (hf) {       // far child: pushed unless it is the only way on
@@ -504,36 +522,28 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
             st_trav_lanes += __popcll(ex);
           }
         }
-        const KNode nd = nodes[node];
-        const f2 t1x = fma2(nd.minx, ix2, lox), t2x = fma2(nd.maxx, ix2, hix);
-        const f2 t1y = fma2(nd.miny, iy2, loy), t2y = fma2(nd.maxy, iy2, hiy);
-        const f2 t1z = fma2(nd.minz, iz2, loz), t2z = fma2(nd.maxz, iz2, hiz);
-        const float tn0 = fmaxf(fmaxf(fminf(t1x.x, t2x.x), fminf(t1y.x, t2y.x)), fminf(t1z.x, t2z.x));
-        const float tf0 = fminf(fminf(fmaxf(t1x.x, t2x.x), fmaxf(t1y.x, t2y.x)), fmaxf(t1z.x, t2z.x));
-        const float tn1 = fmaxf(fmaxf(fminf(t1x.y, t2x.y), fminf(t1y.y, t2y.y)), fminf(t1z.y, t2z.y));
-        const float tf1 = fminf(fminf(fmaxf(t1x.y, t2x.y), fmaxf(t1y.y, t2y.y)), fmaxf(t1z.y, t2z.y));
-        // [tn, tf] meets (tmin, best_t] (tmin < best_t always; a NaN bound only
-        // makes the test pass: conservative)
-        bool hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
-        bool hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
+        float tn0, tn1;
+        bool hit0, hit1;
+        int c0, c1;
+        node_test(node, tn0, tn1, hit0, hit1, c0, c1);
         // leaf children are tested now; a lane's first leaf shares one pass
         // with every other lane's first leaf, whichever child it is
-        const bool l0 = hit0 & (nd.c0 < 0), l1 = hit1 & (nd.c1 < 0);
+        const bool l0 = hit0 & (c0 < 0), l1 = hit1 & (c1 < 0);
         if (l0 | l1) {
-          leaf(l0 ? ~nd.c0 : ~nd.c1);
-          if (l0 & l1) leaf(~nd.c1);
+          leaf(l0 ? ~c0 : ~c1);
+          if (l0 & l1) leaf(~c1);
         }
         hit0 = hit0 & !l0;
         hit1 = hit1 & !l1;
         if (hit0 && hit1) {
           const bool sw = tn1 < tn0;
-          s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? nd.c0 : nd.c1);
+          s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? c0 : c1);
           ++sp;
-          node = sw ? nd.c1 : nd.c0;
+          node = sw ? c1 : c0;
         } else if (hit0) {
-          node = nd.c0;
+          node = c0;
         } else if (hit1) {
-          node = nd.c1;
+          node = c1;
         } else {
           if (sp == 0) break;
           --sp;
