@@ -186,15 +186,16 @@ int rt_set_variant(int variant);
  * result.  Returns the previous value. */
 int rt_set_lanes_per_pixel(int lpp);
 
-/* Diagnostic counters of the stats variants (3, 6, 7, 10, 13) since the last
+/* Diagnostic counters of the stats variants (3, 6, 7, 10, 13, 15, 17) since the last
  * call (then cleared), 16 values: [0] wave loop iterations, [1] active lanes
  * summed over them, [2] body tests per wave (scan) / node visits per lane
  * (BVH), [3] candidate blocks per wave (scan) / leaf tests per lane (BVH),
  * [4] lanes in candidate blocks / exact body tests (BVH), [5] waves,
  * [6] BVH wave-level traversal iterations, [7] lanes active in them,
  * [8..11] shader clocks per wave spent in camera sampling, hit search,
- * shading, accumulation (s_memtime; summed over waves).  Synchronises the
- * device. */
+ * shading, accumulation (s_memtime; summed over waves), [12] BVH
+ * wave-level leaf passes, [13] wave-level exact-test passes.  Synchronises
+ * the device. */
 int rt_debug_stats(uint64_t* out16);
 
 /* Diagnostic wave timeline of variant 3's last launches: n_waves x

@@ -97,11 +97,54 @@ struct Builder {
     return ~p;   // < 0: leaf (its first pair)
   }
 
-  // returns a child ref (node index >= 0, or ~leaf) and its box
-  int build(int lo, int hi, int depth, Box* box) {
-    max_depth = std::max(max_depth, depth);
-    const int cnt = hi - lo;
-    if (cnt <= leaf_size) return leaf(lo, cnt, box);
+  bool sah = true;          // surface-area split (else median)
+
+  static double area(const Box& b) {
+    const double dx = double(b.hi[0]) - b.lo[0], dy = double(b.hi[1]) - b.lo[1], dz = double(b.hi[2]) - b.lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+
+  // orders prim[lo, hi) and returns the split point: the surface-area
+  // heuristic (cost = sum over the two sides of box area x leaf count, all
+  // cut points on all three axes) while the remaining depth allows, else the
+  // median of the widest centroid extent on a leaf-size boundary
+  int split(int lo, int hi, int depth) {
+    const int cnt = hi - lo, L = leaf_size;
+    auto by_axis = [&](int axis) {
+      return [this, axis](int a, int b) {
+        const float ca = sph[4 * a + axis], cb = sph[4 * b + axis];
+        return ca < cb || (ca == cb && a < b);
+      };
+    };
+    // levels a median split below here would still need
+    int need = 0;
+    for (int leaves = (cnt + L - 1) / L; leaves > 1; leaves = (leaves + 1) / 2) ++need;
+    if (sah && depth + need + 3 <= kBvhStack - 2) {
+      double best = INFINITY;
+      int best_axis = 0, best_i = cnt / 2;
+      std::vector<int> ord(prim.begin() + lo, prim.begin() + hi);
+      std::vector<double> right(cnt + 1, 0.0);
+      for (int axis = 0; axis < 3; ++axis) {
+        std::sort(ord.begin(), ord.end(), by_axis(axis));
+        Box r;
+        for (int i = cnt - 1; i >= 1; --i) {
+          r.add(body_box(sph + 4 * ord[i]));
+          right[i] = area(r) * ((cnt - i + L - 1) / L);
+        }
+        Box l;
+        for (int i = 1; i < cnt; ++i) {
+          l.add(body_box(sph + 4 * ord[i - 1]));
+          const double c = area(l) * ((i + L - 1) / L) + right[i];
+          if (c < best) {
+            best = c;
+            best_axis = axis;
+            best_i = i;
+          }
+        }
+      }
+      std::sort(prim.begin() + lo, prim.begin() + hi, by_axis(best_axis));
+      return lo + best_i;
+    }
     Box cb;  // centroid bounds
     for (int i = lo; i < hi; ++i) {
       const float* s = sph + 4 * prim[i];
@@ -114,14 +157,19 @@ struct Builder {
     for (int k = 1; k < 3; ++k)
       if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
     // median split on a leaf-size boundary: balanced depth, full leaves
-    const int L = leaf_size;
     int mid = lo + ((cnt / 2 + L / 2) / L) * L;
     if (mid <= lo) mid = lo + L;
     if (mid >= hi) mid = hi - 1;
-    std::nth_element(prim.begin() + lo, prim.begin() + mid, prim.begin() + hi, [&](int a, int b) {
-      const float ca = sph[4 * a + axis], cb_ = sph[4 * b + axis];
-      return ca < cb_ || (ca == cb_ && a < b);
-    });
+    std::nth_element(prim.begin() + lo, prim.begin() + mid, prim.begin() + hi, by_axis(axis));
+    return mid;
+  }
+
+  // returns a child ref (node index >= 0, or ~leaf) and its box
+  int build(int lo, int hi, int depth, Box* box) {
+    max_depth = std::max(max_depth, depth);
+    const int cnt = hi - lo;
+    if (cnt <= leaf_size) return leaf(lo, cnt, box);
+    const int mid = split(lo, hi, depth);
     const int me = static_cast<int>(out->nodes.size());
     out->nodes.emplace_back();
     Box b0, b1;
@@ -140,7 +188,7 @@ struct Builder {
 
 }  // namespace
 
-int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size) {
+int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size, bool sah) {
   *out = BvhHost{};
   if (leaf_size != 2 && leaf_size != 4) leaf_size = 2;
   out->leaf_size = leaf_size;
@@ -155,6 +203,7 @@ int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size) {
   }
   Builder b{sph, {}, out};
   b.leaf_size = leaf_size;
+  b.sah = sah;
   for (int i = 0; i < n; ++i) {
     const bool finite = std::isfinite(sph[4 * i]) && std::isfinite(sph[4 * i + 1]) &&
                         std::isfinite(sph[4 * i + 2]) && std::isfinite(sph[4 * i + 3]);
@@ -188,32 +237,14 @@ int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size) {
     c0 = c1 = b.leaf(0, 0, &b0);
     for (int k = 0; k < 3; ++k) b0.lo[k] = b0.hi[k] = 0.0f;
     b1 = b0;
+  } else if (cnt <= leaf_size) {
+    c0 = c1 = b.leaf(0, cnt, &b0);   // the same leaf twice: a repeat test never wins a tie
+    b1 = b0;
   } else {
-    const int L = leaf_size;
-    int mid = ((cnt / 2 + L / 2) / L) * L;
-    if (mid <= 0) mid = L;
-    if (mid >= cnt) mid = cnt - 1;
-    // split the root by the same rule as build() (axis from centroid bounds)
-    if (cnt <= L) {
-      c0 = c1 = b.leaf(0, cnt, &b0);   // the same leaf twice: a repeat test never wins a tie
-      b1 = b0;
-    } else {
-      Box cb;
-      for (int i : b.prim)
-        for (int k = 0; k < 3; ++k) {
-          cb.lo[k] = std::min(cb.lo[k], sph[4 * i + k]);
-          cb.hi[k] = std::max(cb.hi[k], sph[4 * i + k]);
-        }
-      int axis = 0;
-      for (int k = 1; k < 3; ++k)
-        if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
-      std::nth_element(b.prim.begin(), b.prim.begin() + mid, b.prim.end(), [&](int x, int y) {
-        const float cx = sph[4 * x + axis], cy = sph[4 * y + axis];
-        return cx < cy || (cx == cy && x < y);
-      });
-      c0 = b.build(0, mid, 1, &b0);
-      c1 = b.build(mid, cnt, 1, &b1);
-    }
+    // the root splits by the same rule as build()
+    const int mid = b.split(0, cnt, 0);
+    c0 = b.build(0, mid, 1, &b0);
+    c1 = b.build(mid, cnt, 1, &b1);
   }
   BvhNode& root = out->nodes[0];
   set_box(root, 0, b0);

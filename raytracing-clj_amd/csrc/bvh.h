@@ -26,10 +26,12 @@ struct BvhHost {
   int leaf_size = 2;          // bodies per leaf (2: one pair, 4: two pairs)
 };
 
-int bvh_build(const float* sphere, int n, BvhHost* out, int leaf_size = 2);
-
-// traversal stack entries per lane (node indices); trees are median-split, so
-// depth <= ceil(log2(n/2)) + 1 (13 for 8192 bodies)
+// traversal stack entries per lane (node indices); the build keeps
+// depth + 2 <= kBvhStack (surface-area splits where the depth allows, median
+// splits below: depth <= ceil(log2(n/2)) + 1 = 13 for 8192 bodies)
 constexpr int kBvhStack = 16;
+
+// sah: surface-area-heuristic splits (else median splits)
+int bvh_build(const float* sphere, int n, BvhHost* out, int leaf_size = 2, bool sah = true);
 
 }  // namespace rtclj

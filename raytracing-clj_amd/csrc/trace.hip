@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   static_assert(LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel");
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
+  uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
@@ -386,7 +388,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
       // size 4), tested packed; the acceptance is order-independent
       auto leaf = [&](int p) {
-        if constexpr (STATS) ++st_blk;
+        if constexpr (STATS) {
+          ++st_blk;
+          const uint64_t ex = __builtin_amdgcn_read_exec();
+          if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_leafw;
+        }
         constexpr int NP = SCAN == SCAN_BVHQ ? 2 : 1;
         float hh[2 * NP], dd[2 * NP];
         int ii[2 * NP];
@@ -411,6 +417,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // one pass of the exact test per candidate: the wave runs it as often
         // as its lane with the most candidates needs (not once per body)
         while (m) {
+          if constexpr (STATS) {
+            const uint64_t ex = __builtin_amdgcn_read_exec();
+            if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_consw;
+          }
           const unsigned k = __builtin_ctz(m);
           m &= m - 1;
           float h = hh[0], d = dd[0];
@@ -809,6 +819,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[6], static_cast<unsigned long long>(st_trav));
       atomicAdd(&a.dbg[7], static_cast<unsigned long long>(st_trav_lanes));
     }
+    if (a.dbg && (st_leafw | st_consw)) {
+      atomicAdd(&a.dbg[12], static_cast<unsigned long long>(st_leafw));
+      atomicAdd(&a.dbg[13], static_cast<unsigned long long>(st_consw));
+    }
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
@@ -922,6 +936,11 @@ static int choose_lpp(int width, int rows, int spp, bool have_all) {
   return 4;
 }
 static int g_variant = 0;
+// BVH build: surface-area splits (default) or median splits (RTCLJ_BVH=median, for A/B)
+static const bool g_bvh_sah = [] {
+  const char* e = std::getenv("RTCLJ_BVH");
+  return !(e && std::strcmp(e, "median") == 0);
+}();
 static unsigned long long* g_dbg = nullptr;   // device u64[8] for variant 3 (per process, device 0)
 static unsigned long long* g_dbgw = nullptr;  // device u64[4 * 65536] wave timeline for variant 3
 
@@ -1026,7 +1045,7 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
   // BVHs over the bodies (the traversal variants): blob = nodes | pairs | pidx
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {
     BvhHost bvh;
-    bvh_build(s->sphere, n, &bvh, k == 0 ? 2 : 4);
+    bvh_build(s->sphere, n, &bvh, k == 0 ? 2 : 4, g_bvh_sah);
     const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
     const size_t pb = bvh.pairs.size() * sizeof(float);
     const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;

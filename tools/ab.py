@@ -85,7 +85,11 @@ def main():
             print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
                               "bvh_considers_per_segment": blk_lanes / segs_total,
                               "trav_wave_iters_per_wave_iter": tw / it, "trav_lane_eff": tl / max(64 * tw, 1),
-                              "trav_lanes_active_frac_of_loop_lanes": tl / max(tw * (lanes / it), 1)}))
+                              "trav_lanes_active_frac_of_loop_lanes": tl / max(tw * (lanes / it), 1),
+                              "leaf_passes_per_trav_iter": stats["dbg"][12] / max(tw, 1),
+                              "exact_passes_per_trav_iter": stats["dbg"][13] / max(tw, 1),
+                              "lanes_per_leaf_pass": blk / max(stats["dbg"][12], 1),
+                              "lanes_per_exact_pass": blk_lanes / max(stats["dbg"][13], 1)}))
         info = {"wave_iters": it, "simd_eff_loop": lanes / (64 * it), "iters_per_wave": it / waves,
                 "block_rate": blk / max(sph, 1), "lanes_per_block": blk_lanes / max(blk, 1), "waves": waves}
         wv = stats["waves"]
