@@ -107,14 +107,14 @@ def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
 
 
 # traversal variant -> (its stats build, body pairs per leaf)
-BVH_STATS = {0: (17, 2), 16: (17, 2), 17: (17, 2), 11: (13, 1), 13: (13, 1), 14: (15, 1), 15: (15, 1)}
+BVH_STATS = {0: (17, 2), 16: (17, 2), 17: (17, 2), 18: (19, 4), 19: (19, 4), 11: (13, 1), 13: (13, 1), 14: (15, 1), 15: (15, 1)}
 
 
 def bvh_counters(ds, cam, p, out, counters, sh, variant):
     """One untimed launch of the stats build of the same frame and traversal
     (variant 17 for the default 16, 13 for 11): per-segment node visits,
     leaf pair tests, exact tests (rt_debug_stats)."""
-    sv, pairs_per_leaf = BVH_STATS[variant]
+    sv, pairs_per_leaf = BVH_STATS[lib.rt_resolve_variant(ds)]
     old = lib.rt_set_variant(sv)
     try:
         dbg = (C.c_uint64 * 16)()
@@ -241,7 +241,8 @@ def main():
         local_stats, tot = ls.cpu(), tt.cpu()
     elapsed, kern_max_ms, kern_avg_ms = local_stats.tolist()
     segs_total, samples_total = tot.tolist()
-    bvh = bvh_counters(ds, cam, p, out, counters, sh, a.variant) if rank == 0 and a.variant in BVH_STATS else None
+    bvh = (bvh_counters(ds, cam, p, out, counters, sh, a.variant)
+           if rank == 0 and lib.rt_resolve_variant(ds) in BVH_STATS else None)
     lib.rt_scene_free(ds)
 
     if rank == 0:

@@ -168,8 +168,10 @@ int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
 
 /* Kernel variant selector for A/B measurement (all variants give identical
- * bits): 0 = default (16); 16 = BVH traversal, 4 bodies per leaf, nodes and
- * leaf bodies in LDS, 17 = 16 with statistics; 11 = the same with 2 bodies
+ * bits): 0 = default (16, or 18 when the 4-body tree's LDS image exceeds
+ * 32 KB and the 8-body tree's is smaller); 16 = BVH traversal, 4 bodies per
+ * leaf, nodes and leaf bodies in LDS, 17 = 16 with statistics, 18 / 19 = the
+ * same with 8 bodies per leaf; 11 = the same with 2 bodies
  * per leaf, 12 = 11 reading the tree from global memory (used when a tree
  * does not fit LDS), 13 = 11 with statistics, 14 / 15 = 11 with a
  * speculative while-while traversal (+ statistics); 1 = sphere table in LDS, one body per step;
@@ -180,6 +182,11 @@ int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
  * (diagnostic builds; slower).  Returns the previous value; applies to
  * subsequent launches in this process. */
 int rt_set_variant(int variant);
+
+/* The kernel variant rt_launch would run for ds under the current selector
+ * (the default resolved for this scene, or a fallback when a tree does not
+ * fit): for reading the matching statistics build.  -1 on a NULL scene. */
+int rt_resolve_variant(const rt_dscene* ds);
 
 /* Lanes per pixel (1, 2, 4; 0 = automatic by frame size): how many lanes
  * share one pixel's four sample stripes.  Changes the launch shape, never the

@@ -72,7 +72,7 @@ struct Builder {
   BvhHost* out;
   int max_depth = 0;
 
-  int leaf_size = 2;       // bodies per leaf: 2 (one pair) or 4 (two pairs)
+  int leaf_size = 2;       // bodies per leaf: 2, 4 or 8 (1, 2 or 4 pairs)
 
   int leaf(int lo, int cnt, Box* box) {
     const int p = static_cast<int>(out->pidx.size() / 2);
@@ -190,7 +190,7 @@ struct Builder {
 
 int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size, bool sah) {
   *out = BvhHost{};
-  if (leaf_size != 2 && leaf_size != 4) leaf_size = 2;
+  if (leaf_size != 2 && leaf_size != 4 && leaf_size != 8) leaf_size = 2;
   out->leaf_size = leaf_size;
   // big bodies: scanned first, outside the tree
   std::vector<float> radii;

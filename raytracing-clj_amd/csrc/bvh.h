@@ -23,7 +23,7 @@ struct BvhHost {
   float center[3] = {0, 0, 0};
   float radius = 0.0f;        // bounding sphere of the tree's bodies
   int depth = 0;              // levels of nodes on the longest root-leaf path
-  int leaf_size = 2;          // bodies per leaf (2: one pair, 4: two pairs)
+  int leaf_size = 2;          // bodies per leaf (2, 4 or 8: 1, 2 or 4 pairs)
 };
 
 // traversal stack entries per lane (node indices); the build keeps

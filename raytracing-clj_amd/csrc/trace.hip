@@ -126,9 +126,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
-enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4, SCAN_BVHQ = 5 };
+enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4, SCAN_BVHQ = 5, SCAN_BVHO = 6 };
 // the traversal variants (BVHQ: ordered traversal of the 4-body-leaf tree)
-constexpr bool is_bvh_scan(int scan) { return scan == SCAN_BVH || scan == SCAN_BVHWW || scan == SCAN_BVHQ; }
+constexpr bool is_bvh_scan(int scan) { return scan >= SCAN_BVH && scan <= SCAN_BVHO; }
+// body pairs per leaf of the tree a traversal variant walks
+constexpr int leaf_pairs(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_BVHQ ? 2 : 1; }
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           const uint64_t ex = __builtin_amdgcn_read_exec();
           if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_leafw;
         }
-        constexpr int NP = SCAN == SCAN_BVHQ ? 2 : 1;
+        constexpr int NP = leaf_pairs(SCAN);
         float hh[2 * NP], dd[2 * NP];
         int ii[2 * NP];
         unsigned m = 0;   // candidate bodies of the leaf
@@ -871,8 +873,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 //  11 BVH in LDS                  12 BVH in global memory   13 = 11 + stats
 //  14 BVH in LDS, speculative while-while traversal          15 = 14 + stats
 //  16 BVH in LDS, 4-body leaves (two pairs)                  17 = 16 + stats
+//  18 BVH in LDS, 8-body leaves (four pairs)                 19 = 18 + stats
 //     (BVH variants fall back to 5 when the tree does not fit / is too deep)
-//   0 = default (16)
+//   0 = default (16, or 18 when the 4-body tree's LDS image is large)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
 // 0 = automatic (enough waves to keep the chip full to the end).
 struct Variant {
@@ -880,7 +883,9 @@ struct Variant {
   bool lds;
   bool stats;
 };
-constexpr int kVariants = 18;
+constexpr int kVariants = 20;
+// the tree a traversal variant walks: 0 = 2-body leaves, 1 = 4, 2 = 8
+static int variant_tree(int v) { return v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 #define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
 static const Variant& variant_table(int v) {
   static const Variant t[kVariants] = {
@@ -917,6 +922,10 @@ static const Variant& variant_table(int v) {
         RT_K(SRC_LDS, SCAN_BVHQ, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHQ, 1, true), RT_K(SRC_LDS, SCAN_BVHQ, 2, true),
         RT_K(SRC_LDS, SCAN_BVHQ, 4, true)}, true, true},
+      {{RT_K(SRC_LDS, SCAN_BVHO, 1, false), RT_K(SRC_LDS, SCAN_BVHO, 2, false),
+        RT_K(SRC_LDS, SCAN_BVHO, 4, false)}, true, false},
+      {{RT_K(SRC_LDS, SCAN_BVHO, 1, true), RT_K(SRC_LDS, SCAN_BVHO, 2, true),
+        RT_K(SRC_LDS, SCAN_BVHO, 4, true)}, true, true},
   };
   return t[(v >= 0 && v < kVariants) ? v : 0];
 }
@@ -962,8 +971,8 @@ struct rt_dscene {
   int n_pad;
   float4* geo;
   float4* geo2;   // n_pad/2 Pairs (= n_pad float4)
-  // BVHs (bvh.cpp): tree[0] 2-body leaves, tree[1] 4-body leaves
-  DTree tree[2];
+  // BVHs (bvh.cpp): tree[0] 2-body leaves, tree[1] 4-body, tree[2] 8-body
+  DTree tree[3];
   float4* sph;
   float4* mat;
   int* kind;
@@ -1043,9 +1052,9 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
   d->n_pad = n_pad;
   hipError_t e = hipMalloc(&d->geo, n_pad * sizeof(float4));
   // BVHs over the bodies (the traversal variants): blob = nodes | pairs | pidx
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) {
     BvhHost bvh;
-    bvh_build(s->sphere, n, &bvh, k == 0 ? 2 : 4, g_bvh_sah);
+    bvh_build(s->sphere, n, &bvh, 2 << k, g_bvh_sah);
     const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
     const size_t pb = bvh.pairs.size() * sizeof(float);
     const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;
@@ -1101,6 +1110,26 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   return RT_OK;
 }
 
+static size_t stack_of(const DTree& t) { return static_cast<size_t>(t.depth + 2) * 256 * sizeof(unsigned short); }
+static size_t lds_of(const DTree& t) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t); }
+
+// selector -> the variant a launch on ds runs
+static int resolve_variant(const rt_dscene& ds, int vsel) {
+  // default: 4-body leaves, unless that tree's LDS image limits a CU below
+  // the 5 workgroups the registers allow (160 KB / 5) and the 8-body-leaf
+  // tree's is smaller (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
+  if (vsel == 0) vsel = (lds_of(ds.tree[1]) > 32 * 1024 && lds_of(ds.tree[2]) < lds_of(ds.tree[1])) ? 18 : 16;
+  if (vsel >= 11) {
+    const DTree& t = ds.tree[variant_tree(vsel)];
+    if (t.depth + 2 > kBvhStack) return 5;                       // tree too deep for the stack
+    if (vsel != 12 && lds_of(t) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
+    if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
+  }
+  return vsel;
+}
+
+extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_variant(*ds, g_variant) : -1; }
+
 extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p, float* d_out,
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();
@@ -1138,17 +1167,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
-  int vsel = g_variant;
-  if (vsel == 0) vsel = 16;
-  auto stack_of = [](const DTree& t) { return static_cast<size_t>(t.depth + 2) * 256 * sizeof(unsigned short); };
-  auto lds_of = [&](const DTree& t) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t); };
-  if (vsel >= 11) {
-    const DTree& t = ds->tree[vsel >= 16 ? 1 : 0];
-    if (t.depth + 2 > kBvhStack) vsel = 5;                      // tree too deep for the stack
-    else if (vsel != 12 && lds_of(t) > 96 * 1024) vsel = 12;    // tree too big for LDS: 2-body leaves, global
-  }
-  const DTree& tr = ds->tree[vsel >= 16 ? 1 : 0];
-  if (vsel == 12 && tr.depth + 2 > kBvhStack) vsel = 5;
+  const int vsel = resolve_variant(*ds, g_variant);
+  const DTree& tr = ds->tree[variant_tree(vsel)];
   const size_t stack_bytes = stack_of(tr);
   const size_t bvh_lds = lds_of(tr);
   const Variant& v = variant_table(vsel);

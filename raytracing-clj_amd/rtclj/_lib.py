@@ -74,6 +74,7 @@ SIGNATURES = {
     "rt_launch": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_params), C.c_void_p,
                             C.c_void_p, C.c_void_p]),
     "rt_set_variant": (C.c_int, [C.c_int]),
+    "rt_resolve_variant": (C.c_int, [C.c_void_p]),
     "rt_set_lanes_per_pixel": (C.c_int, [C.c_int]),
     "rt_debug_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
     "rt_debug_waves": (C.c_int, [C.POINTER(C.c_uint64), C.c_size_t]),

@@ -120,3 +120,4 @@ def test_version_and_variant():
     old = rtclj.lib.rt_set_variant(2)
     assert rtclj.lib.rt_set_variant(old) == 2
     assert rtclj.lib.rt_set_variant(99) == old   # ignored
+    assert rtclj.lib.rt_resolve_variant(None) == -1

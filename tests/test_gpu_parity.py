@@ -161,7 +161,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 @pytest.mark.parametrize("lpp", [1, 2, 4])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
@@ -176,7 +176,7 @@ def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     try:
         st = {}
         g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7, 10, 13, 15, 17):
+        if variant in (3, 6, 7, 10, 13, 15, 17, 19):
             import ctypes as C
             d = (C.c_uint64 * 16)()
             lib.rt_debug_stats(d)
@@ -280,7 +280,7 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("variant", [11, 12, 14, 16])
+@pytest.mark.parametrize("variant", [11, 12, 14, 16, 18])
 def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
@@ -341,7 +341,7 @@ def test_bvh_small_scenes(gpu_lib, n):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
     out = {}
-    for v in (5, 11, 16):
+    for v in (5, 11, 16, 18):
         old = lib.rt_set_variant(v)
         try:
             out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5)
@@ -349,11 +349,12 @@ def test_bvh_small_scenes(gpu_lib, n):
             lib.rt_set_variant(old)
     assert np.array_equal(out[5], out[11])
     assert np.array_equal(out[5], out[16])
+    assert np.array_equal(out[5], out[18])
     ref, _, _ = _mirror(sc, cam, 48, 27, 8, 20, seed=5)
     assert np.array_equal(out[5], ref)
 
 
-@pytest.mark.parametrize("variant", [11, 16])
+@pytest.mark.parametrize("variant", [0, 11, 16, 18])
 def test_bvh_large_scene_falls_back(gpu_lib, variant):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
     the global-memory traversal of the 2-body tree: same bits as the scan."""

@@ -58,7 +58,7 @@ def main():
             elif not np.array_equal(img, ref):
                 print(f"variant {name}: frame differs from variant {names[0]}!", flush=True)
                 sys.exit(1)
-            if v in (3, 6, 7, 10, 13, 15, 17):
+            if v in (3, 6, 7, 10, 13, 15, 17, 19):
                 d = (C.c_uint64 * 16)()
                 check(lib.rt_debug_stats(d))
                 d = list(d)
@@ -80,7 +80,7 @@ def main():
     if "dbg" in stats:
         it, lanes, sph, blk, blk_lanes, waves = stats["dbg"][:6]
         segs_total = stats[names[0]]["segments"]
-        if stats["dbg_variant"].split(":")[0] in ("13", "15", "17"):
+        if stats["dbg_variant"].split(":")[0] in ("13", "15", "17", "19"):
             tw, tl = stats["dbg"][6], stats["dbg"][7]
             print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
                               "bvh_considers_per_segment": blk_lanes / segs_total,
