@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4; big-body scan test = 16
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16b"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16c"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -99,11 +99,22 @@ def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
                 break
     except OSError:
         pass
+    # the reference's own setting: a pool of 2 threads (raytracing.clj:157),
+    # on a 16x sparser row sample (about the same CPU time)
+    step2 = row_step * 16
+    t1 = time.perf_counter()
+    _, _, _, samples2 = oracle.render(oracle.MODE_REF64, scene.sphere.astype(np.float64), scene.kind,
+                                      scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
+                                      seed=seed, row_step=step2, nthreads=min(2, nthreads))
+    dt2 = time.perf_counter() - t1
     return {"value": samples / dt / 1e6, "unit": "Mray-samples/s", "cores": nthreads, "kind": "port",
             "sample": f"rows 0,{row_step},{2 * row_step},... ({rows} rows x {w} px x {spp} spp = {samples} samples) "
                       f"of the same frame, fp64 reference semantics (oracle MODE_REF64), {dt:.1f} s",
             "seconds": dt, "segments_per_sample": segs / max(samples, 1), "cpu_model": cpu,
-            "host": platform.node()}
+            "host": platform.node(),
+            "two_threads": {"value": samples2 / dt2 / 1e6, "cores": min(2, nthreads),
+                            "sample": f"every {step2}th row ({samples2} samples), {dt2:.1f} s: the reference's "
+                                      f"pool-size 2 (raytracing.clj:157)"}}
 
 
 # traversal variant -> (its stats build, body pairs per leaf)
@@ -131,22 +142,49 @@ def bvh_counters(ds, cam, p, out, counters, sh, variant):
             "stats_variant": sv}
 
 
-def pmc_traffic(kernel_substr="trace_kernel"):
+def _pmc_avg(passes, counters):
+    """Per-dispatch averages of PMC counters over the timed kernel's launches
+    (trace_kernel, not its stats build) in the committed rocprofv3 passes."""
+    import csv
+    acc = {}
+    for name in passes:
+        f = PMC_DEFAULT / f"{name}.csv"
+        if not f.exists():
+            return None
+        for r in csv.DictReader(open(f)):
+            if "trace_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"] and r["Counter_Name"] in counters:
+                acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if any(c not in acc for c in counters):
+        return None
+    return {c: sum(v) / len(v) for c, v in acc.items()}
+
+
+def pmc_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC passes (separate
     FETCH_SIZE / WRITE_SIZE runs, KB units; gfx950 FETCH_SIZE counts half the
     bytes of wide streaming reads -> x2, MI355X_MICROARCH.md §HBM)."""
-    import csv
-    vals = {}
-    for name in ("fetch", "write"):
-        f = PMC_DEFAULT / f"{name}.csv"
-        if not f.exists():
-            return None, None
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-             if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE")]
-        if not v:
-            return None, None
-        vals[name] = sum(v) / len(v) * 1024.0
-    return 2.0 * vals["fetch"] + vals["write"], str(PMC_DEFAULT.relative_to(ROOT))
+    v = _pmc_avg(("fetch", "write"), ("FETCH_SIZE", "WRITE_SIZE"))
+    if v is None:
+        return None, None
+    return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(PMC_DEFAULT.relative_to(ROOT))
+
+
+def pmc_valu(n_simd=1024, n_xcd=8):
+    """VALU issue picture of the same launches: the fraction of cycles each
+    SIMD issues a VALU instruction (SQ_ACTIVE_INST_VALU, 4-cycle units,
+    summed over the SIMDs, vs GRBM_GUI_ACTIVE summed over the XCDs) and the
+    mean fraction of the 64 lanes active per VALU instruction."""
+    v = _pmc_avg(("insts", "waves"), ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU",
+                                      "GRBM_GUI_ACTIVE"))
+    if v is None:
+        return None
+    busy = v["SQ_ACTIVE_INST_VALU"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
+    lanes = v["SQ_THREAD_CYCLES_VALU"] / v["SQ_INSTS_VALU"] / 64.0
+    return {"issue_busy": busy, "lanes_active": lanes, "valu_insts": v["SQ_INSTS_VALU"],
+            "source": str(PMC_DEFAULT.relative_to(ROOT)),
+            "note": "the binding limit: VALU issue slots (a wave64 instruction takes 4 cycles whatever its "
+                    "active lanes); executed-flop frac = issue_busy x lanes_active x (flops per issued "
+                    "lane-instruction)"}
 
 
 def main():
@@ -287,6 +325,7 @@ def main():
             "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
+            "valu": pmc_valu(),
             "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
