@@ -39,7 +39,7 @@ typedef enum rt_status {
   RT_E_TOO_MANY = -3,   /* sphere list larger than the LDS-resident limit        */
   RT_E_HIP = -4,        /* HIP runtime error (message has the HIP error string)  */
   RT_E_NODEV = -5,      /* no GPU visible / device index out of range            */
-  RT_E_IO = -6          /* file I/O (rt_write_ppm)                               */
+  RT_E_IO = -6          /* file I/O (rt_write_ppm, rt_write_png, rt_ppm_to_png)  */
 } rt_status;
 
 /* ---- material kinds: material.clj:13 (lambertian), :21 (metal), :34 (dielectric).
@@ -94,13 +94,22 @@ typedef struct rt_params {
   int row_tile;           /* interleaved tile height (rows); 0 -> 8            */
   int tile_first;         /* rt_launch: first tile of this shard               */
   int tile_step;          /* rt_launch: tile stride (0 = contiguous rows)      */
-  int flags;              /* 0, or RT_FLAG_SHARDS_ON_DEVICE0                   */
+  int flags;              /* 0, RT_FLAG_REALM, RT_FLAG_SHARDS_ON_DEVICE0 (ored) */
 } rt_params;
 
 /* rt_render: split into n_devices interleaved-tile shards exactly as for n
  * GPUs, but run every shard on device 0 (exercises the multi-GPU fan-out and
  * host gather on a one-GPU machine).  n_devices must be > 0. */
 #define RT_FLAG_SHARDS_ON_DEVICE0 1
+
+/* rt_launch / rt_render: the semantics of the reference's second namespace,
+ * realm.raytracing (`clojure -M:realm`, src/realm/raytracing.clj) instead of
+ * raytracing (`-M:main`): lambertian scatter without the near-zero fallback
+ * (:137-143), dielectric without Schlick reflectance and its draw (:158-177),
+ * and the pixel as sum * (1/spp) rather than sum / spp (:25, :276).  Its
+ * camera (no defocus, focal length |lookfrom - lookat|) is an rt_camera like
+ * any other (rt_camera_setup with defocus_angle 0). */
+#define RT_FLAG_REALM 2
 
 /* ---- per-call statistics (device-side counters) ------------------------- */
 typedef struct rt_stats {
@@ -128,6 +137,15 @@ int rt_quantize(const float* lin, uint8_t* out, size_t n);
 
 /* PPM P3, one "r g b\n" per pixel, rows top->bottom (raytracing.clj:172-175). */
 int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
+
+/* PNG, 8-bit truecolour RGB, adaptive per-row filters, deflate: the same
+ * pixels as rt_write_ppm (the format src/ppm2png.clj:35-87 converts to). */
+int rt_write_png(const char* path, const uint8_t* rgb, int width, int height);
+
+/* ppm->png (src/ppm2png.clj:35-87): read a P3 file (max value <= 255, w*h
+ * pixels of 3 values) and write it as rt_write_png does.  RT_E_ARG on a
+ * malformed PPM, RT_E_IO on file errors. */
+int rt_ppm_to_png(const char* src_ppm, const char* dst_png);
 
 /* Number of output rows a (row_begin,row_end,row_tile,tile_first,tile_step)
  * selection produces (0 on bad args). */

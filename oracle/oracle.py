@@ -15,7 +15,7 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "_build" / "liboracle.so"
-MODE_REF64, MODE_MIRROR32, MODE_BOOK64 = 0, 1, 2
+MODE_REF64, MODE_MIRROR32, MODE_BOOK64, MODE_REALM64, MODE_REALM32 = 0, 1, 2, 3, 4
 
 _dll = None
 

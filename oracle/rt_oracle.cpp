@@ -23,6 +23,17 @@
 //     summed in min(4, spp) contiguous stripes then ((s0+s1)+s2)+s3.  The
 //     GPU output must equal this bit for bit.
 //
+//   MODE_REALM64 (3) — the reference's second namespace, realm.raytracing
+//     (src/realm/raytracing.clj, `clojure -M:realm`), in double: the same
+//     hit test and samplers, but lambertian without the near-zero fallback
+//     (:137-143), dielectric without Schlick reflectance, i.e. no draw
+//     (:160-177), an iterative ray-color that multiplies the throughput
+//     forward (:205-236), and the pixel as sum * (1/spp) (:25, :276).
+//     Its camera (no defocus, focal length |lookfrom - lookat|, :285-300) is
+//     the caller's rt_camera.
+//   MODE_REALM32 (4) — MODE_MIRROR32 with the kernel's RT_FLAG_REALM: the
+//     same three semantic changes, the pixel as total * RN(1/spp).
+//
 // The reference's RNG is clojure.core/rand (unseeded java.util.Random,
 // vec3a.clj:71-72), so no bitwise reference image exists.  Both modes draw
 // from the build's keyed stream instead: xorshift32 seeded per
@@ -44,7 +55,7 @@
 
 namespace {
 
-enum { MODE_REF64 = 0, MODE_MIRROR32 = 1, MODE_BOOK64 = 2 };
+enum { MODE_REF64 = 0, MODE_MIRROR32 = 1, MODE_BOOK64 = 2, MODE_REALM64 = 3, MODE_REALM32 = 4 };
 
 // MODE_BOOK64: MODE_REF64 but metal reflects unit(d) as the RTIOW book does
 // (negative control: scene.ppm must reject it).
@@ -229,6 +240,54 @@ V ray_color64(const Scene64& sc, V o, V d, int depth, Rng& rng, uint64_t* segs) 
   return vadd(vmul(V{1.0, 1.0, 1.0}, 1.0 - a), vmul(V{0.5, 0.7, 1.0}, a));
 }
 
+// realm/raytracing.clj:205-236: iterative; target starts at (1,1,1) and is
+// multiplied by each attenuation, then by the sky colour (:229-236)
+V ray_color_realm64(const Scene64& sc, V o, V d, int depth, Rng& rng, uint64_t* segs) {
+  V target{1.0, 1.0, 1.0};
+  for (;;) {
+    if (depth <= 0) return V{0, 0, 0};
+    Hit64 h;
+    if (!hit_anything64(sc, o, d, 1e-3, INFINITY, &h, segs)) {
+      const double y = vunit(d).y;
+      const double a = 0.5 * (y + 1.0);
+      const V sky{(1.0 - a) * 1.0 + a * 0.5, (1.0 - a) * 1.0 + a * 0.7, (1.0 - a) * 1.0 + a * 1.0};
+      return vmulv(target, sky);
+    }
+    const double* m = sc.mat + 4 * h.what;
+    const V alb{m[0], m[1], m[2]};
+    V sd, att;
+    switch (sc.kind[h.what]) {
+      case LAMB:  // :137-143, no near-zero fallback
+        sd = vadd(random_unit64(rng), h.n);
+        att = alb;
+        break;
+      case METAL: {  // :145-156
+        const V refl = reflect64(d, h.n);
+        const V r2 = vadd(refl, vmul(random_unit64(rng), m[3]));
+        if (!(vdot(r2, h.n) > 0)) return V{0, 0, 0};
+        sd = r2;
+        att = alb;
+        break;
+      }
+      case NONE:
+        return V{0, 0, 0};
+      default: {  // :158-177, no Schlick term and no draw
+        const double ri = h.front ? (1.0 / m[3]) : m[3];
+        const V u = vunit(d);
+        const double cs = std::min(vdot(vneg(u), h.n), 1.0);
+        const double sn = std::sqrt(1.0 - cs * cs);
+        sd = ri * sn > 1.0 ? reflect64(u, h.n) : refract64(u, h.n, ri);
+        att = V{1.0, 1.0, 1.0};
+        break;
+      }
+    }
+    target = vmulv(target, att);
+    o = h.p;
+    d = sd;
+    --depth;
+  }
+}
+
 // ---------------------------------------------------------- fp32 mirror ---
 struct Scene32 {
   int n;
@@ -253,7 +312,7 @@ void random_unit32(Rng& s, float& x, float& y, float& z) {
 }
 
 // one sample of the stackless kernel loop; returns colour, adds segments
-void sample32(const Scene32& sc, const float* cam, bool defocus, int px, int gy, uint32_t st,
+void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int px, int gy, uint32_t st,
               int max_depth, float* col, uint64_t* segs) {
   Rng rng{st};
   const float fx = static_cast<float>(px) + (rng.uf() - 0.5f);
@@ -338,7 +397,7 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, int px, int gy,
       float rx, ry, rz;
       random_unit32(rng, rx, ry, rz);
       float qx = rx + nx, qy = ry + ny, qz = rz + nz;
-      if (std::fabs(qx) < 1e-8f && std::fabs(qy) < 1e-8f && std::fabs(qz) < 1e-8f) {
+      if (!realm && std::fabs(qx) < 1e-8f && std::fabs(qy) < 1e-8f && std::fabs(qz) < 1e-8f) {
         qx = nx;
         qy = ny;
         qz = nz;
@@ -370,7 +429,7 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, int px, int gy,
       const float cosv = std::fmin(-un, 1.0f);
       const float sinv = std::sqrt(std::fmaf(-cosv, cosv, 1.0f));
       bool refl = !(ri * sinv <= 1.0f);
-      if (!refl) {
+      if (!refl && !realm) {
         const float xi = rng.uf();
         float r0 = (1.0f - ri) / (1.0f + ri);
         r0 = r0 * r0;
@@ -413,10 +472,11 @@ struct Job {
 void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
   const int gy = J.row_begin + ro * J.row_step;
   t_book_metal = J.mode == MODE_BOOK64;
+  const bool realm = J.mode == MODE_REALM64 || J.mode == MODE_REALM32;
   for (int px = x0; px < x1; ++px) {
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(J.width) + static_cast<uint32_t>(px);
     const size_t o = (static_cast<size_t>(ro) * J.width + px) * 3;
-    if (J.mode == MODE_REF64 || J.mode == MODE_BOOK64) {
+    if (J.mode == MODE_REF64 || J.mode == MODE_BOOK64 || J.mode == MODE_REALM64) {
       // compute-pixel (raytracing.clj:141-155)
       const double* c = J.cam64;
       const V center{c[0], c[1], c[2]}, p00{c[3], c[4], c[5]}, du{c[6], c[7], c[8]}, dv{c[9], c[10], c[11]};
@@ -434,9 +494,12 @@ void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
           org = vadd(vadd(center, vmul(disk_u, p.x)), vmul(disk_v, p.y));
         }
         const V dir = vsub(ps, org);
-        acc = vadd(acc, ray_color64(J.s64, org, dir, J.max_depth, rng, segs));
+        acc = vadd(acc, realm ? ray_color_realm64(J.s64, org, dir, J.max_depth, rng, segs)
+                              : ray_color64(J.s64, org, dir, J.max_depth, rng, segs));
       }
-      const V res = vdiv(acc, static_cast<double>(J.spp));
+      // compute-pixel divides by spp (raytracing.clj:155); realm multiplies
+      // by pixel-scale = 1.0 / spp (realm/raytracing.clj:25, :276)
+      const V res = realm ? vmul(acc, 1.0 / static_cast<double>(J.spp)) : vdiv(acc, static_cast<double>(J.spp));
       J.out[o] = static_cast<float>(res.x);
       J.out[o + 1] = static_cast<float>(res.y);
       J.out[o + 2] = static_cast<float>(res.z);
@@ -460,7 +523,7 @@ void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
           uint32_t st = mix32(pk + static_cast<uint32_t>(J.sample_begin + k) * 0x9e3779b9u);
           if (st == 0) st = 0x6d2b79f5u;
           float col[3];
-          sample32(J.s32, J.cam32, J.defocus, px, gy, st, J.max_depth, col, segs);
+          sample32(J.s32, J.cam32, J.defocus, realm, px, gy, st, J.max_depth, col, segs);
           ar += col[0];
           ag += col[1];
           ab += col[2];
@@ -470,9 +533,16 @@ void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
         tb_ += ab;
       }
       const float inv = static_cast<float>(J.spp);
-      J.out[o] = tr_ / inv;
-      J.out[o + 1] = tg_ / inv;
-      J.out[o + 2] = tb_ / inv;
+      if (realm) {  // total * RN(1/spp)
+        const float sc = 1.0f / inv;
+        J.out[o] = tr_ * sc;
+        J.out[o + 1] = tg_ * sc;
+        J.out[o + 2] = tb_ * sc;
+      } else {
+        J.out[o] = tr_ / inv;
+        J.out[o + 1] = tg_ / inv;
+        J.out[o + 2] = tb_ / inv;
+      }
     }
   }
 }
@@ -492,7 +562,7 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
                   float* out, double* out64, uint64_t* counters) {
   if (width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_end < row_begin || !out ||
       row_step <= 0 ||
-      (n > 0 && (!sphere || !kind || !mat)) || !cam || mode < MODE_REF64 || mode > MODE_BOOK64)
+      (n > 0 && (!sphere || !kind || !mat)) || !cam || mode < MODE_REF64 || mode > MODE_REALM32)
     return -1;
   Job J{};
   J.mode = mode;

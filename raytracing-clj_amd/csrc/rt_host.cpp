@@ -222,9 +222,9 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   clear_error();
   const auto t0 = std::chrono::steady_clock::now();
   if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, "rt_render: NULL argument");
-  const bool on_dev0 = p->flags == RT_FLAG_SHARDS_ON_DEVICE0;
+  const bool on_dev0 = (p->flags & RT_FLAG_SHARDS_ON_DEVICE0) != 0;
   if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->n_devices < 0 ||
-      (p->flags != 0 && !on_dev0) || (on_dev0 && p->n_devices == 0))
+      (p->flags & ~(RT_FLAG_SHARDS_ON_DEVICE0 | RT_FLAG_REALM)) != 0 || (on_dev0 && p->n_devices == 0))
     return set_error(RT_E_ARG, "rt_render: bad width/height/spp/flags/n_devices");
   if (p->tile_step != 0 || p->tile_first != 0)
     return set_error(RT_E_ARG, "rt_render: tile_first/tile_step are per-shard (rt_launch) fields");
@@ -248,7 +248,7 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     Shard& sh = shards[d];
     sh.device = on_dev0 ? 0 : d;
     sh.p = *p;
-    sh.p.flags = 0;
+    sh.p.flags = p->flags & RT_FLAG_REALM;   // semantics travel; the fan-out flag is rt_render's
     sh.p.row_tile = T;
     if (ndev > 1) {
       sh.p.tile_first = d;

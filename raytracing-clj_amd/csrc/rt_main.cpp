@@ -1,15 +1,22 @@
 // rt_main — C++ host driver mirroring `clojure -M:main [spp] [depth]`
 // (src/raytracing.clj:95-177): prints the config, renders the reference's
 // five-body scene at 400x225 through rt_render, writes scene.ppm.
+// --realm mirrors `clojure -M:realm` (src/realm/raytracing.clj:279-359)
+// instead: realm's body order, camera (no defocus, focal length
+// |look-from - look-at|), height (int (/ ^double 400 ^double 16/9)) = 224 and
+// RT_FLAG_REALM semantics; it writes scene-realm.ppm.  --png also writes the
+// frame as a PNG (rt_write_png; what src/ppm2png.clj produces).
 //
-//   rt_main [spp] [depth] [--scene reference|cover] [--width W] [--seed S]
-//           [--gpus N] [--out PATH]
+//   rt_main [spp] [depth] [--scene reference|cover] [--realm] [--width W]
+//           [--seed S] [--gpus N] [--out PATH] [--png PATH]
 // Defaults follow the reference: spp 100, depth 50, width 400, 16:9.
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rt.h"
@@ -17,7 +24,8 @@
 int main(int argc, char** argv) {
   int spp = 100, depth = 50, width = 400, gpus = 0, grid = 11;
   unsigned long long seed = 1;
-  std::string scene = "reference", out = "scene.ppm";
+  std::string scene = "reference", out, png;
+  bool realm = false;
   int pos = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -34,11 +42,17 @@ int main(int argc, char** argv) {
     else if (a == "--gpus") gpus = std::atoi(val());
     else if (a == "--grid") grid = std::atoi(val());
     else if (a == "--out") out = val();
+    else if (a == "--png") png = val();
+    else if (a == "--realm") realm = true;
     else if (pos == 0) spp = std::atoi(argv[i]), ++pos;   // (:96)
     else if (pos == 1) depth = std::atoi(argv[i]), ++pos; // (:97)
   }
-  std::printf("config: {:samples-per-px %d, :max-depth %d}\n", spp, depth);  // (:98)
-  const int height = width * 9 / 16;  // (int (/ image-width 16/9)) (:105-107)
+  if (out.empty()) out = realm ? "scene-realm.ppm" : "scene.ppm";
+  if (!realm) std::printf("config: {:samples-per-px %d, :max-depth %d}\n", spp, depth);  // (:98)
+  // -main: (int (/ image-width 16/9)) in exact ratios (:105-107); realm: a
+  // double division by Ratio.doubleValue(16/9) = 1.777777777777778
+  // (realm/raytracing.clj:20-22), 400 -> 224
+  const int height = realm ? static_cast<int>(width / 1.777777777777778) : width * 9 / 16;
   const int cap = RT_MAX_SPHERES;
   std::vector<float> sph(4 * cap), mat(4 * cap);
   std::vector<int> kind(cap);
@@ -51,7 +65,18 @@ int main(int argc, char** argv) {
   } else {
     n = rt_scene_reference(sph.data(), kind.data(), mat.data(), cap);
     const double lf[3] = {-2, 2, 1}, la[3] = {0, 0, -1}, up[3] = {0, 1, 0};  // (:110-115)
-    rt_camera_setup(width, height, 20.0, lf, la, up, 10.0, 3.4, &cam);
+    if (realm) {
+      // realm/raytracing.clj:307-317 lists the centre sphere before the ground
+      for (int k = 0; k < 4; ++k) {
+        std::swap(sph[k], sph[4 + k]);
+        std::swap(mat[k], mat[4 + k]);
+      }
+      std::swap(kind[0], kind[1]);
+      const double fl = std::sqrt(4.0 + 4.0 + 4.0);   // |look-from - look-at| (:291-292)
+      rt_camera_setup(width, height, 20.0, lf, la, up, 0.0, fl, &cam);
+    } else {
+      rt_camera_setup(width, height, 20.0, lf, la, up, 10.0, 3.4, &cam);
+    }
   }
   rt_scene s{n, sph.data(), kind.data(), mat.data()};
   rt_params p{};
@@ -63,6 +88,7 @@ int main(int argc, char** argv) {
   p.max_depth = depth;
   p.seed = seed;
   p.n_devices = gpus;
+  p.flags = realm ? RT_FLAG_REALM : 0;
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<float> lin(static_cast<size_t>(width) * height * 3);
   rt_stats st{};
@@ -72,7 +98,8 @@ int main(int argc, char** argv) {
   }
   std::vector<uint8_t> q(lin.size());
   rt_quantize(lin.data(), q.data(), q.size());
-  if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK) {
+  if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK ||
+      (!png.empty() && rt_write_png(png.c_str(), q.data(), width, height) != RT_OK)) {
     std::fprintf(stderr, "%s\n", rt_last_error());
     return 1;
   }

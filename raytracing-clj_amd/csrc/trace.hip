@@ -73,6 +73,7 @@ struct alignas(16) KArgs {
   int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   int spp, sample_begin, max_depth;
+  int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
 };
 
@@ -686,7 +687,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         if (kind == RT_LAMBERTIAN) {
           // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
           float sx = qx + nx, sy = qy + ny, sz = qz + nz;
-          if (fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {
+          // (realm.raytracing has no near-zero fallback, realm/raytracing.clj:137-143)
+          if (!a.realm && fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {
             sx = nx;
             sy = ny;
             sz = nz;
@@ -722,7 +724,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const float cosv = fminf(-un, 1.0f);
         const float sinv = sqrtf(fmaf(-cosv, cosv, 1.0f));
         bool refl = !(ri * sinv <= 1.0f);
-        if (!refl) {
+        if (!refl && !a.realm) {   // (realm: no Schlick term, no draw; realm/raytracing.clj:158-177)
           const float xi = rng_uniform(st);  // drawn only when refraction is possible
           float r0 = (1.0f - ri) / (1.0f + ri);
           r0 = r0 * r0;
@@ -806,9 +808,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if (in_image && grp == 0) {
     const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
     float* o = a.out + (static_cast<size_t>(ro) * a.width + px) * 3;
-    o[0] = outr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
-    o[1] = outg / inv;
-    o[2] = outb / inv;
+    if (a.realm) {
+      const float sc = 1.0f / inv;   // pixel-scale (realm/raytracing.clj:25, :276)
+      o[0] = outr * sc;
+      o[1] = outg * sc;
+      o[2] = outb * sc;
+    } else {
+      o[0] = outr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
+      o[1] = outg / inv;
+      o[2] = outb / inv;
+    }
   }
 
   if constexpr (STATS) {
@@ -1134,7 +1143,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();
   if (!ds || !c || !p || !d_out) return set_error(RT_E_ARG, "rt_launch: NULL argument");
-  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->flags != 0)
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || (p->flags & ~RT_FLAG_REALM) != 0)
     return set_error(RT_E_ARG, "rt_launch: bad width/height/spp/flags");
   const int rows = rows_out(*p);
   if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
@@ -1164,6 +1173,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.spp = p->spp;
   a.sample_begin = p->sample_begin;
   a.max_depth = p->max_depth;
+  a.realm = (p->flags & RT_FLAG_REALM) ? 1 : 0;
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));

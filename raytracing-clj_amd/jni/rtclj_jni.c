@@ -8,9 +8,14 @@
  *                            float[] camera, int defocus, int width, int height,
  *                            int spp, int depth, long seed, int nGpus,
  *                            float[] outRgb);
+ *   static native int renderWithFlags(... the same ..., int nGpus, int flags,
+ *                                     float[] outRgb);   // RT_FLAG_REALM: -M:realm
  *   static native int deviceCount();
+ *   static native int writePng(String path, byte[] rgb, int width, int height);
+ *   static native int ppmToPng(String srcPpm, String dstPng);
  * camera = 18 floats: center, p00, du, dv, disk_u, disk_v (rt_camera order).
- * Replaces compute-pixel + the executor (src/raytracing.clj:141-171).
+ * Replaces compute-pixel + the executor (src/raytracing.clj:141-171) and
+ * ppm2png/ppm->png (src/ppm2png.clj:35-87).
  */
 #include <jni.h>
 #include <stdio.h>
@@ -33,11 +38,9 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_deviceCount(JNIEnv* env, jclass cls) {
   return rt_device_count();
 }
 
-JNIEXPORT jint JNICALL Java_rtclj_Native_render(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
-                                                jfloatArray mats, jfloatArray camera, jint defocus, jint width,
-                                                jint height, jint spp, jint depth, jlong seed, jint n_gpus,
-                                                jfloatArray out_rgb) {
-  (void)cls;
+static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloatArray mats, jfloatArray camera,
+                        jint defocus, jint width, jint height, jint spp, jint depth, jlong seed, jint n_gpus,
+                        jint flags, jfloatArray out_rgb) {
   const jsize n = (*env)->GetArrayLength(env, kinds);
   if ((*env)->GetArrayLength(env, spheres) != 4 * n || (*env)->GetArrayLength(env, mats) != 4 * n ||
       (*env)->GetArrayLength(env, camera) != 18) {
@@ -70,12 +73,59 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_render(JNIEnv* env, jclass cls, jfloatA
   p.max_depth = depth;
   p.seed = (uint64_t)seed;
   p.n_devices = n_gpus;
+  p.flags = flags;
   float* out = (float*)(*env)->GetPrimitiveArrayCritical(env, out_rgb, NULL);
   const int rc = rt_render(&scene, &cam, &p, out, (size_t)out_len, NULL);
   (*env)->ReleasePrimitiveArrayCritical(env, out_rgb, out, 0);
   (*env)->ReleaseFloatArrayElements(env, spheres, (jfloat*)sph, JNI_ABORT);
   (*env)->ReleaseIntArrayElements(env, kinds, knd, JNI_ABORT);
   (*env)->ReleaseFloatArrayElements(env, mats, (jfloat*)mat, JNI_ABORT);
+  if (rc < 0) throw_rt(env, rc);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_render(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
+                                                jfloatArray mats, jfloatArray camera, jint defocus, jint width,
+                                                jint height, jint spp, jint depth, jlong seed, jint n_gpus,
+                                                jfloatArray out_rgb) {
+  (void)cls;
+  return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, 0,
+                     out_rgb);
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls, jfloatArray spheres,
+                                                         jintArray kinds, jfloatArray mats, jfloatArray camera,
+                                                         jint defocus, jint width, jint height, jint spp,
+                                                         jint depth, jlong seed, jint n_gpus, jint flags,
+                                                         jfloatArray out_rgb) {
+  (void)cls;
+  return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, flags,
+                     out_rgb);
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_writePng(JNIEnv* env, jclass cls, jstring path, jbyteArray rgb, jint width,
+                                                  jint height) {
+  (void)cls;
+  if ((jlong)(*env)->GetArrayLength(env, rgb) < (jlong)width * height * 3) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
+  const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+  jbyte* px = (*env)->GetByteArrayElements(env, rgb, NULL);
+  const int rc = rt_write_png(p, (const uint8_t*)px, width, height);
+  (*env)->ReleaseByteArrayElements(env, rgb, px, JNI_ABORT);
+  (*env)->ReleaseStringUTFChars(env, path, p);
+  if (rc < 0) throw_rt(env, rc);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_ppmToPng(JNIEnv* env, jclass cls, jstring src, jstring dst) {
+  (void)cls;
+  const char* s = (*env)->GetStringUTFChars(env, src, NULL);
+  const char* d = (*env)->GetStringUTFChars(env, dst, NULL);
+  const int rc = rt_ppm_to_png(s, d);
+  (*env)->ReleaseStringUTFChars(env, dst, d);
+  (*env)->ReleaseStringUTFChars(env, src, s);
   if (rc < 0) throw_rt(env, rc);
   return rc;
 }

@@ -32,12 +32,26 @@
 
 (defn render
   "width*height*3 linear RGB floats: compute-pixel's accum/spp for every pixel.
-  camera keys are the values -main derives (raytracing.clj:126-139)."
+  camera keys are the values -main derives (raytracing.clj:126-139).
+  :realm? true renders with realm.raytracing's semantics (RT_FLAG_REALM:
+  src/realm/raytracing.clj; pass realm's camera: no defocus, focal length
+  |look-from - look-at|)."
   [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
-   {:keys [width height samples-per-px max-depth seed gpus] :or {seed 1 gpus 0}}]
+   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
   (let [[sph knd mat] (flatten-bodies bodies)
         cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))
         out (float-array (* width height 3))]
-    (Native/render sph knd mat cam (if (pos? defocus-angle) 1 0) width height
-                   samples-per-px max-depth (long seed) (int gpus) out)
+    (Native/renderWithFlags sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
+                            samples-per-px max-depth (long seed) (int gpus)
+                            (if realm? Native/FLAG_REALM 0) out)
     out))
+
+(defn write-png!
+  "rgb: width*height*3 bytes (write-color!'s 0..255 values) -> PNG file."
+  [path ^bytes rgb width height]
+  (Native/writePng (str path) rgb (int width) (int height)))
+
+(defn ppm->png
+  "src/ppm2png.clj:35-87's ppm->png through the library."
+  [source dest]
+  (Native/ppmToPng (str source) (str dest)))

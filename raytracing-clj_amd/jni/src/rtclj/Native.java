@@ -13,5 +13,18 @@ public final class Native {
                                   int width, int height, int spp, int depth, long seed, int nGpus,
                                   float[] outRgb);
 
+  /** render with rt_params.flags (RT_FLAG_REALM = 2: the realm.raytracing semantics). */
+  public static native int renderWithFlags(float[] spheres, int[] kinds, float[] mats, float[] camera,
+                                           int defocus, int width, int height, int spp, int depth, long seed,
+                                           int nGpus, int flags, float[] outRgb);
+
+  public static final int FLAG_REALM = 2;
+
   public static native int deviceCount();
+
+  /** 8-bit RGB PNG of width x height x 3 bytes (rt_write_png). */
+  public static native int writePng(String path, byte[] rgb, int width, int height);
+
+  /** ppm2png/ppm->png (src/ppm2png.clj:35-87) through rt_ppm_to_png. */
+  public static native int ppmToPng(String srcPpm, String dstPng);
 }

@@ -17,6 +17,7 @@ RT_OK, RT_E_ARG, RT_E_MATERIAL, RT_E_TOO_MANY, RT_E_HIP, RT_E_NODEV, RT_E_IO = 0
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_NONE = 0, 1, 2, 3
 RT_MAX_SPHERES = 8192
 RT_FLAG_SHARDS_ON_DEVICE0 = 1
+RT_FLAG_REALM = 2
 
 
 class RTError(RuntimeError):
@@ -63,6 +64,8 @@ SIGNATURES = {
                                   C.POINTER(C.c_double), C.c_double, C.c_double, C.POINTER(rt_camera)]),
     "rt_quantize": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.c_size_t]),
     "rt_write_ppm": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    "rt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    "rt_ppm_to_png": (C.c_int, [C.c_char_p, C.c_char_p]),
     "rt_rows_out": (C.c_int, [C.POINTER(rt_params)]),
     "rt_scene_reference": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int]),
     "rt_scene_cover": (C.c_int, [C.c_int, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_int),

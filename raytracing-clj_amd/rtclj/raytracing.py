@@ -6,6 +6,8 @@
                                            on the GPU(s) via rt_render
     write_color     raytracing.clj:19-26   gamma-2, clamp 0.999, x256
     write_ppm       raytracing.clj:172-175 P3, one pixel per line
+    write_png,      ppm2png.clj:35-87      8-bit RGB PNG of the same pixels
+      ppm_to_png
     main            raytracing.clj:95-177  `clojure -M:main [spp] [depth]`
 
 The per-pixel loop (compute-pixel -> ray-color -> hit-anything -> hit-fn /
@@ -154,6 +156,19 @@ def write_ppm(path, rgb8) -> None:
     check(lib.rt_write_ppm(str(path).encode(), u8ptr(rgb8), w, h))
 
 
+def write_png(path, rgb8) -> None:
+    """The same pixels as write_ppm, as an 8-bit RGB PNG (rt_write_png; the
+    format src/ppm2png.clj produces)."""
+    rgb8 = np.ascontiguousarray(rgb8, np.uint8)
+    h, w = rgb8.shape[:2]
+    check(lib.rt_write_png(str(path).encode(), u8ptr(rgb8), w, h))
+
+
+def ppm_to_png(src, dst) -> None:
+    """ppm2png/ppm->png (src/ppm2png.clj:35-87) via rt_ppm_to_png."""
+    check(lib.rt_ppm_to_png(str(src).encode(), str(dst).encode()))
+
+
 def read_ppm(path) -> np.ndarray:
     """Parse a P3 file (as written by write_ppm or the reference) -> uint8 (H, W, 3)."""
     tok = open(path).read().split()
@@ -190,4 +205,4 @@ if __name__ == "__main__":  # python -m rtclj.raytracing [spp] [depth]
 
 
 __all__ = ["hittables", "REFERENCE_CAMERA", "image_height", "flatten", "flatten64", "Scene", "camera", "render",
-           "write_color", "write_ppm", "read_ppm", "main", "dptr"]
+           "write_color", "write_ppm", "write_png", "ppm_to_png", "read_ppm", "main", "dptr"]

@@ -13,7 +13,14 @@ where /root/reference exists; nothing at test time reads /root/reference).
   rng_golden.json        the keyed RNG contract (lowbias32 + xorshift32),
                          computed here in pure Python
   mirror_small.npz       small renders by the oracle's fp32 kernel mirror
-                         (regression pins for the oracle and the GPU path)
+                         (regression pins for the oracle and the GPU path),
+                         incl. one in realm semantics (MODE_REALM32)
+  scene_realm_ppm.npz    the reference's realm.raytracing output,
+  scene_realm_ppm_stats.json   scene-realm.ppm (`clojure -M:realm`: 400x225,
+                         100 spp, depth 50), pixels and the same statistics
+  scene_png.json         the reference's scene.png (ppm2png output), decoded
+                         by tests/pngdec.py: header, row filters, sha256 of
+                         the decoded pixels, and whether they equal scene.ppm's
 
 Usage: python tests/golden/make_golden.py
 """
@@ -30,6 +37,8 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent.parent
 REF_PPM = Path("/root/reference/scene.ppm")
+REF_REALM_PPM = Path("/root/reference/scene-realm.ppm")
+REF_PNG = Path("/root/reference/scene.png")
 M32 = 0xFFFFFFFF
 
 
@@ -250,6 +259,28 @@ def main():
         print("scene.ppm", img.shape, st["mean"])
     else:
         print("no /root/reference/scene.ppm here: keeping the committed scene fixtures")
+    if REF_REALM_PPM.exists():
+        img = read_p3(REF_REALM_PPM)
+        np.savez_compressed(HERE / "scene_realm_ppm.npz", pixels=img)
+        st = image_stats(img)
+        st["source"] = ("reference scene-realm.ppm (clojure -M:realm output; 400x225, 100 spp, depth 50: "
+                        "realm/raytracing.clj:20-24)")
+        st["sha256"] = hashlib.sha256(REF_REALM_PPM.read_bytes()).hexdigest()
+        (HERE / "scene_realm_ppm_stats.json").write_text(json.dumps(st, indent=1))
+        print("scene-realm.ppm", img.shape, st["mean"])
+    if REF_PNG.exists() and REF_PPM.exists():
+        sys.path.insert(0, str(HERE.parent))
+        import pngdec
+        px, info = pngdec.decode(REF_PNG.read_bytes())
+        ppm = read_p3(REF_PPM)
+        rec = {k: info[k] for k in ("width", "height", "depth", "color_type", "interlace")}
+        rec.update(source="reference scene.png (ppm2png output of scene.ppm, src/ppm2png.clj:35-87)",
+                   png_sha256=hashlib.sha256(REF_PNG.read_bytes()).hexdigest(),
+                   row_filter_counts={str(f): info["row_filters"].count(f) for f in sorted(set(info["row_filters"]))},
+                   decoded_rgb_sha256=hashlib.sha256(np.ascontiguousarray(px[..., :3]).tobytes()).hexdigest(),
+                   equals_scene_ppm=bool(px.shape[:2] == ppm.shape[:2] and np.array_equal(px[..., :3], ppm)))
+        (HERE / "scene_png.json").write_text(json.dumps(rec, indent=1))
+        print("scene.png", rec)
     (HERE / "kats.json").write_text(json.dumps(kats(), indent=1))
     rng = [{"seed": s, "pixel": p, "sample": k, "draws": stream(s, p, k, 8)}
            for s, p, k in [(1, 0, 0), (1, 0, 1), (1, 1, 0), (7, 12345, 99), (2**40 + 3, 810000 - 1, 1999)]]
@@ -267,8 +298,13 @@ def main():
     cc = scenes.cover_camera(32, 18)
     cov, _, segs_c, _ = oracle.render(oracle.MODE_MIRROR32, cs.sphere.astype(np.float64), cs.kind,
                                       cs.mat.astype(np.float64), cc.as_list(), cc.defocus, 32, 18, 4, 50, seed=5)
+    from rtclj import realm
+    rs = R.Scene.from_bodies(realm.hittables)
+    rc = realm.camera(48, 27)
+    rlm, _, segs_m, _ = oracle.render(oracle.MODE_REALM32, rs.sphere.astype(np.float64), rs.kind,
+                                      rs.mat.astype(np.float64), rc.as_list(), rc.defocus, 48, 27, 8, 50, seed=3)
     np.savez_compressed(HERE / "mirror_small.npz", reference_48x27_spp8_seed3=ref, cover_32x18_spp4_seed5=cov,
-                        segments=np.array([segs_r, segs_c], np.int64))
+                        realm_48x27_spp8_seed3=rlm, segments=np.array([segs_r, segs_c, segs_m], np.int64))
     print("kats, rng, mirror fixtures written")
 
 

@@ -379,3 +379,60 @@ def test_bvh_large_scene_falls_back(gpu_lib, variant):
         finally:
             lib.rt_set_variant(old)
     assert np.array_equal(out[5], out[variant])
+
+
+def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
+    out, _, segs, smp = oracle.render(oracle.MODE_REALM32, scene.sphere.astype(np.float64), scene.kind,
+                                      scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
+                                      seed=seed, rows=rows)
+    return out, segs, smp
+
+
+@pytest.mark.parametrize("variant", [0, 5, 11, 16, 18])
+def test_realm_flag_matches_mirror(gpu_lib, variant):
+    """RT_FLAG_REALM (realm.raytracing semantics) through the kernel == the
+    oracle's MODE_REALM32, bit for bit: the realm scene and the cover scene."""
+    from rtclj import raytracing as R
+    from rtclj import realm, scenes
+    from rtclj._lib import lib
+    cases = [(R.Scene.from_bodies(realm.hittables), realm.camera(48, 27), 48, 27, 8),
+             (scenes.cover(11), scenes.cover_camera(40, 22), 40, 22, 7)]
+    old = lib.rt_set_variant(variant)
+    try:
+        for sc, cam, w, h, spp in cases:
+            st = {}
+            g = realm.render(sc, cam, w, h, spp=spp, max_depth=50, seed=3, stats=st)
+            ref, segs, smp = _realm_mirror(sc, cam, w, h, spp, 50, seed=3)
+            assert np.array_equal(g, ref), (variant, w, h)
+            assert st["segments"] == segs and st["samples"] == smp
+    finally:
+        lib.rt_set_variant(old)
+
+
+def test_realm_shards_and_fixture(gpu_lib):
+    """realm's own frame (400x224, 100 spp, depth 50) on the GPU: sharded ==
+    single, rows bit-exact with the mirror, and the image within the
+    scene-realm.ppm tolerances (tests/test_realm.py)."""
+    import json
+    from pathlib import Path
+    from rtclj import raytracing as R
+    from rtclj import realm
+    from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0
+    sc = R.Scene.from_bodies(realm.hittables)
+    w = 400
+    h = realm.image_height(w)
+    cam = realm.camera(w, h)
+    lin = realm.render(sc, cam, w, h, seed=1)
+    shard = realm.render(sc, cam, w, h, seed=1, n_devices=3, flags=RT_FLAG_SHARDS_ON_DEVICE0)
+    assert np.array_equal(lin, shard)
+    ref, _, _ = _realm_mirror(sc, cam, w, h, 100, 50, seed=1, rows=(100, 104))
+    assert np.array_equal(lin[100:104], ref)
+    g = Path(__file__).parent / "golden"
+    st = json.loads((g / "scene_realm_ppm_stats.json").read_text())
+    pix = np.load(g / "scene_realm_ppm.npz")["pixels"]
+    rgb = R.write_color(lin).astype(np.float64)
+    blocks = np.array([[rgb[y * h // 9:(y + 1) * h // 9, x * w // 16:(x + 1) * w // 16].reshape(-1, 3).mean(0)
+                        for x in range(16)] for y in range(9)])
+    d = np.abs(blocks - np.array(st["blocks"]))
+    assert d.mean() <= 0.25 and d.max() <= 2.5, (d.mean(), d.max())
+    assert np.abs(rgb - pix).mean() <= 3.5
