@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 _PKG_ROOT = Path(__file__).resolve().parent.parent          # raytracing-clj_amd/
-library_path = _PKG_ROOT / "lib" / "librtclj.so"
+# RTCLJ_LIBRARY: load another build of the same ABI (A/B of kernel builds)
+library_path = Path(os.environ["RTCLJ_LIBRARY"]) if os.environ.get("RTCLJ_LIBRARY") else _PKG_ROOT / "lib" / "librtclj.so"
 
 RT_OK, RT_E_ARG, RT_E_MATERIAL, RT_E_TOO_MANY, RT_E_HIP, RT_E_NODEV, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_NONE = 0, 1, 2, 3
