@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4; big-body scan test = 16
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16c"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16d"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp (not a bench line)")
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant)")
     ap.add_argument("--lpp", type=int, default=0, help="lanes per pixel (rt_set_lanes_per_pixel; 0 auto)")
+    ap.add_argument("--schedule", type=int, default=0,
+                    help="tile schedule (rt_set_schedule): 0 adaptive longest-first, 1 plain dispatch order")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -224,6 +226,7 @@ def main():
     red_dev = dev if backend == "nccl" else torch.device("cpu")
     lib.rt_set_variant(a.variant)
     lib.rt_set_lanes_per_pixel(a.lpp)
+    lib.rt_set_schedule(a.schedule)
 
     wl = dict(WORKLOADS[a.workload])
     if a.spp:
@@ -314,7 +317,8 @@ def main():
             "config": {"workload": wl["name"] if not a.spp else f"{wl['name']} (spp override {spp})",
                        "width": W, "height": H, "spp_per_gpu": spp, "max_depth": depth, "bodies": len(scene),
                        "parallelism": ("sample-stripe x%d (weak)" % world) if a.scaling == "weak"
-                       else ("row-tile 8 x%d (strong)" % world), "variant": a.variant},
+                       else ("row-tile 8 x%d (strong)" % world), "variant": a.variant,
+                       "tile_schedule": "adaptive longest-first" if a.schedule == 0 else "dispatch order"},
             "roofline": {"bound": "mfma", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": tflops / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "note": f"compute-bound fp32 on the VALU (branchy per-ray FP work, no GEMM shape: MFMA unused); "

@@ -211,6 +211,19 @@ int rt_resolve_variant(const rt_dscene* ds);
  * result.  Returns the previous value. */
 int rt_set_lanes_per_pixel(int lpp);
 
+/* Tile dispatch order of rt_launch.  0 (default) = adaptive: every launch
+ * records how long each tile's waves ran, and a one-block sort enqueued after
+ * it (same stream, no host sync) turns that into a longest-first order; the
+ * next launch on the same scene and stream with the same launch shape (width,
+ * row selection, kernel variant, lanes per pixel; camera, spp, seed and flags
+ * may differ) dispatches its tiles in that order, so the slow tiles do not
+ * trail the kernel's end.  A launch of another shape runs in plain order and
+ * re-keys the record (per scene, up to 8 streams; launches on further streams
+ * are unscheduled).  1 = always plain order.  Changes timing only: every
+ * pixel is computed the same way in any order (bit-identical output).
+ * Returns the previous value. */
+int rt_set_schedule(int mode);
+
 /* Diagnostic counters of the stats variants (3, 6, 7, 10, 13, 15, 17) since the last
  * call (then cleared), 16 values: [0] wave loop iterations, [1] active lanes
  * summed over them, [2] body tests per wave (scan) / node visits per lane

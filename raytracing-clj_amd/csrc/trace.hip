@@ -37,6 +37,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -72,6 +73,8 @@ struct alignas(16) KArgs {
   int n_big;
   int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
+  const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
+  unsigned* tile_cost;     // nullable: per tile, the longest of its waves' durations (s_memrealtime ticks)
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
-  if constexpr (STATS) st_t0 = __builtin_amdgcn_s_memrealtime();
+  if (STATS || a.tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
   if constexpr (is_bvh_scan(SCAN)) {
@@ -197,8 +200,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int lane = threadIdx.x & 63;
   const int pl = lane % PX;     // pixel within the wave tile
   const int grp = lane / PX;    // stripe group
-  const int px = blockIdx.x * (2 * TW) + (wave & 1) * TW + (pl % TW);
-  const int ro = blockIdx.y * (2 * TH) + (wave >> 1) * TH + (pl / TW);
+  // the block's tile: its dispatch slot, or the tile_order permutation of it
+  const int slot = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
+  const int tile = a.tile_order ? a.tile_order[slot] : slot;
+  const int tbx = tile % static_cast<int>(gridDim.x), tby = tile / static_cast<int>(gridDim.x);
+  const int px = tbx * (2 * TW) + (wave & 1) * TW + (pl % TW);
+  const int ro = tby * (2 * TH) + (wave >> 1) * TH + (pl / TW);
   const bool in_image = (px < a.width) && (ro < a.rows_out);
   bool active = in_image;
 
@@ -820,6 +827,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
   }
 
+  if (a.tile_cost && lane == 0) {   // the adaptive schedule's measurement
+    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - st_t0;
+    atomicMax(&a.tile_cost[tile], static_cast<unsigned>(dt < 0xffffffffull ? dt : 0xffffffffull));
+  }
   if constexpr (STATS) {
     if (a.dbg && st_iter) {
       atomicAdd(&a.dbg[0], static_cast<unsigned long long>(st_iter));
@@ -849,7 +860,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[11], static_cast<unsigned long long>(c3));
     }
     if (a.dbgw && lane == 0) {
-      const size_t wid = (static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6);
+      const size_t wid = static_cast<size_t>(tile) * 4 + (threadIdx.x >> 6);   // by tile
       if (wid < 65536) {
         a.dbgw[4 * wid + 0] = st_t0;
         a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -871,6 +882,34 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.counters[1], static_cast<unsigned long long>(smp));
     }
   }
+}
+
+// The adaptive schedule's sort: tile indices by descending cost (a counting
+// sort over 256 log-scale buckets: the top 5 bits are the cost's bit length,
+// the low 3 the bits below its leading one).  One block; the order within a
+// bucket is arbitrary (any order renders the same bits).
+__device__ __forceinline__ int cost_bucket(unsigned c) {
+  if (c < 8) return static_cast<int>(c);
+  const int e = 31 - __clz(c);                                  // 3..31
+  return ((e - 2) << 3) | static_cast<int>((c >> (e - 3)) & 7u); // monotone, < 256
+}
+__global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict__ cost, int* __restrict__ order,
+                                                     int n) {
+  __shared__ int hist[256];
+  __shared__ int cursor[256];
+  for (int i = threadIdx.x; i < 256; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 1024) atomicAdd(&hist[cost_bucket(cost[i])], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int b = 255; b >= 0; --b) {   // descending cost first
+      cursor[b] = run;
+      run += hist[b];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 1024) order[atomicAdd(&cursor[cost_bucket(cost[i])], 1)] = i;
 }
 
 // ------------------------------------------------------------- host ------
@@ -954,6 +993,8 @@ static int choose_lpp(int width, int rows, int spp, bool have_all) {
   return 4;
 }
 static int g_variant = 0;
+// tile schedule (rt_set_schedule): 0 = adaptive longest-first, 1 = dispatch order
+static int g_schedule = 0;
 // BVH build: surface-area splits (default) or median splits (RTCLJ_BVH=median, for A/B)
 static const bool g_bvh_sah = [] {
   const char* e = std::getenv("RTCLJ_BVH");
@@ -974,6 +1015,40 @@ struct DTree {
   float c[3], r;
 };
 
+// Adaptive tile schedule (rt_launch): per stream, the per-tile durations of
+// the stream's last launch and the longest-first order derived from them, for
+// the launch shape `key` (frame rows, tiling, kernel variant, grid).  The
+// order is a prediction: camera, spp, seed and flags may change between
+// launches of one shape (progressive passes, animation) and it stays a good
+// one, and it never affects the result.  A launch of another shape re-keys the
+// entry (and runs in dispatch order once).  Entries are per stream so that nothing a
+// stream's kernels read is written from another stream; a dscene serves up to
+// kSchedStreams streams this way, launches on further streams run unscheduled.
+struct ScheduleKey {
+  int width, rows, row_begin, row_tile, tile_first, tile_step, variant, lpp, gx, gy;
+};
+struct Schedule {
+  hipStream_t stream = nullptr;
+  unsigned* cost = nullptr;
+  int* order = nullptr;
+  int cap = 0;          // tiles the buffers hold
+  bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
+  ScheduleKey key{};
+};
+constexpr int kSchedStreams = 8;
+struct ScheduleSet {
+  std::mutex mu;
+  int used = 0;
+  Schedule s[kSchedStreams];
+  void release() {
+    for (int k = 0; k < used; ++k) {
+      if (s[k].cost) (void)hipFree(s[k].cost);
+      if (s[k].order) (void)hipFree(s[k].order);
+    }
+    used = 0;
+  }
+};
+
 struct rt_dscene {
   int device;
   int n;
@@ -985,6 +1060,7 @@ struct rt_dscene {
   float4* sph;
   float4* mat;
   int* kind;
+  mutable ScheduleSet sched;   // rt_launch's adaptive tile order
 };
 
 static int hip_fail(hipError_t e, const char* what) {
@@ -1000,6 +1076,12 @@ static int hip_fail(hipError_t e, const char* what) {
 extern "C" int rt_set_variant(int v) {
   const int old = g_variant;
   if (v >= 0 && v < kVariants) g_variant = v;
+  return old;
+}
+
+extern "C" int rt_set_schedule(int mode) {
+  const int old = g_schedule;
+  if (mode == 0 || mode == 1) g_schedule = mode;
   return old;
 }
 
@@ -1112,6 +1194,7 @@ extern "C" int rt_scene_free(rt_dscene* d) {
     if (t.blob) (void)hipFree(t.blob);
     if (t.big) (void)hipFree(t.big);
   }
+  d->sched.release();
   if (d->sph) (void)hipFree(d->sph);
   if (d->mat) (void)hipFree(d->mat);
   if (d->kind) (void)hipFree(d->kind);
@@ -1218,8 +1301,64 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     if (lds > 64 * 1024)
       HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   }
+  // adaptive schedule: dispatch tiles longest first, by the durations the
+  // previous launch of this frame geometry on this scene and stream measured
+  Schedule* sch = nullptr;
+  std::unique_lock<std::mutex> sched_lock;
+  if (g_schedule == 0) {
+    ScheduleKey key{};
+    key.width = a.width;
+    key.rows = a.rows_out;
+    key.row_begin = a.row_begin;
+    key.row_tile = a.row_tile;
+    key.tile_first = a.tile_first;
+    key.tile_step = a.tile_step;
+    key.variant = vsel;
+    key.lpp = lpp;
+    key.gx = static_cast<int>(grid.x);
+    key.gy = static_cast<int>(grid.y);
+    const int n_tiles = key.gx * key.gy;
+    ScheduleSet& set = ds->sched;
+    sched_lock = std::unique_lock<std::mutex>(set.mu);
+    for (int k = 0; k < set.used && !sch; ++k)
+      if (set.s[k].stream == stream) sch = &set.s[k];
+    if (!sch && set.used < kSchedStreams) {
+      sch = &set.s[set.used++];
+      sch->stream = stream;
+    }
+    if (sch && std::memcmp(&sch->key, &key, sizeof key) != 0) {
+      sch->ready = false;
+      sch->key = key;
+    }
+    if (sch && sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->cost) (void)hipFree(sch->cost);
+      if (sch->order) (void)hipFree(sch->order);
+      sch->cost = nullptr;
+      sch->order = nullptr;
+      sch->cap = 0;
+      sch->ready = false;
+      HIP_TRY(hipMalloc(&sch->cost, n_tiles * sizeof(unsigned)));
+      HIP_TRY(hipMalloc(&sch->order, n_tiles * sizeof(int)));
+      sch->cap = n_tiles;
+    }
+    if (sch) {
+      if (sch->ready) a.tile_order = sch->order;
+      a.tile_cost = sch->cost;
+      HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
+    }
+  }
   void* args[] = {&a};
   HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
+  if (sch) {
+    // the next launch's order, stream-ordered after this kernel (no host sync)
+    const unsigned* cost = sch->cost;
+    int* order = sch->order;
+    int n = static_cast<int>(grid.x * grid.y);
+    void* sargs[] = {&cost, &order, &n};
+    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
+    sch->ready = true;
+  }
   HIP_TRY(hipGetLastError());
   return RT_OK;
 }

@@ -80,6 +80,7 @@ SIGNATURES = {
     "rt_set_variant": (C.c_int, [C.c_int]),
     "rt_resolve_variant": (C.c_int, [C.c_void_p]),
     "rt_set_lanes_per_pixel": (C.c_int, [C.c_int]),
+    "rt_set_schedule": (C.c_int, [C.c_int]),
     "rt_debug_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
     "rt_debug_waves": (C.c_int, [C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_device_count": (C.c_int, []),

@@ -121,3 +121,10 @@ def test_version_and_variant():
     assert rtclj.lib.rt_set_variant(old) == 2
     assert rtclj.lib.rt_set_variant(99) == old   # ignored
     assert rtclj.lib.rt_resolve_variant(None) == -1
+
+
+def test_schedule_switch():
+    import rtclj
+    assert rtclj.lib.rt_set_schedule(1) == 0      # adaptive is the default
+    assert rtclj.lib.rt_set_schedule(7) == 1      # ignored
+    assert rtclj.lib.rt_set_schedule(0) == 1

@@ -1,0 +1,148 @@
+"""The adaptive tile schedule (rt_set_schedule, include/rt.h): rt_launch on a
+persistent scene dispatches tiles longest first by the previous launch's
+durations.  The order must be a permutation of the launch's tiles and never
+change a bit of the output: every launch here writes into a NaN-filled buffer
+(a tile skipped or run twice would leave NaNs or be caught by the equality)
+and is compared with rt_render of the same frame (fresh scene: plain order),
+itself pinned to the oracle by test_gpu_parity.py.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env(gpu_lib):
+    import torch
+    from rtclj import scenes
+    from rtclj._lib import check, lib
+    sc = scenes.cover(11)
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    yield sc, ds, torch
+    lib.rt_scene_free(ds)
+
+
+def _launch(env, cam, w, h, spp, stream=None, seed=1, rows=None, row_tile=0, tile_first=0, tile_step=0,
+            sample_begin=0):
+    sc, ds, torch = env
+    from rtclj._lib import check, lib, rt_params
+    r0, r1 = rows or (0, h)
+    p = rt_params(width=w, height=h, row_begin=r0, row_end=r1, spp=spp, max_depth=50, seed=seed,
+                  sample_begin=sample_begin, row_tile=row_tile, tile_first=tile_first, tile_step=tile_step)
+    n = check(lib.rt_rows_out(C.byref(p)))
+    s = stream or torch.cuda.current_stream()
+    with torch.cuda.stream(s):
+        out = torch.full((n * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
+    s.synchronize()
+    check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), None,
+                        C.c_void_p(s.cuda_stream)))
+    s.synchronize()
+    return out.cpu().numpy().reshape(n, w, 3)
+
+
+def _render(sc, cam, w, h, spp, **kw):
+    from rtclj import raytracing as R
+    return R.render(sc, cam, w, h, spp=spp, max_depth=50, **kw)
+
+
+@pytest.mark.parametrize("variant,lpp", [(0, 0), (0, 1), (0, 4), (11, 0), (18, 2), (5, 0)])
+def test_repeated_launches_are_bit_identical(env, variant, lpp):
+    from rtclj import scenes
+    from rtclj._lib import lib
+    sc = env[0]
+    w, h, spp = 333, 187, 6                       # ragged tiles at both edges
+    cam = scenes.cover_camera(w, h)
+    ov, ol = lib.rt_set_variant(variant), lib.rt_set_lanes_per_pixel(lpp)
+    try:
+        want = _render(sc, cam, w, h, spp)
+        for k in range(4):                        # launch 0 plain, then scheduled by the previous launch
+            got = _launch(env, cam, w, h, spp)
+            assert not np.isnan(got).any(), k
+            assert np.array_equal(got, want), k
+    finally:
+        lib.rt_set_variant(ov)
+        lib.rt_set_lanes_per_pixel(ol)
+
+
+def test_schedule_off_matches_on(env):
+    from rtclj import scenes
+    from rtclj._lib import lib
+    w, h, spp = 256, 144, 8
+    cam = scenes.cover_camera(w, h)
+    on = [_launch(env, cam, w, h, spp) for _ in range(2)]
+    old = lib.rt_set_schedule(1)
+    try:
+        off = _launch(env, cam, w, h, spp)
+    finally:
+        lib.rt_set_schedule(old)
+    assert np.array_equal(on[0], off) and np.array_equal(on[1], off)
+
+
+def test_same_shape_other_camera_seed_and_samples(env):
+    """The order recorded for one frame is reused by the next launch of the
+    same shape with another camera, seed and sample range: still exact."""
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = env[0]
+    w, h = 200, 112
+    cam_a = scenes.cover_camera(w, h)
+    cam_b = R.camera(w, h, 30.0, (10.0, 3.0, -4.0), (0.0, 0.5, 0.0), (0.0, 1.0, 0.0), 0.0, 10.0)
+    _launch(env, cam_a, w, h, 4)
+    got = _launch(env, cam_b, w, h, 5, seed=7)
+    assert np.array_equal(got, _render(sc, cam_b, w, h, 5, seed=7))
+    got = _launch(env, cam_b, w, h, 4, seed=7, sample_begin=4)
+    assert np.array_equal(got, _render(sc, cam_b, w, h, 4, seed=7, sample_begin=4))
+
+
+def test_shape_changes_and_row_shards(env):
+    """Alternating shapes re-key the record; interleaved row-tile shards (the
+    multi-GPU split) keep their own tile count."""
+    from rtclj import scenes
+    sc = env[0]
+    for w, h in ((160, 90), (96, 54), (160, 90), (1, 1), (160, 90)):
+        cam = scenes.cover_camera(w, h)
+        assert np.array_equal(_launch(env, cam, w, h, 3), _render(sc, cam, w, h, 3)), (w, h)
+    w, h = 180, 101
+    cam = scenes.cover_camera(w, h)
+    full = _render(sc, cam, w, h, 4)
+    for _ in range(2):
+        parts = [_launch(env, cam, w, h, 4, row_tile=8, tile_first=f, tile_step=3) for f in range(3)]
+        for f, part in enumerate(parts):
+            rows = np.concatenate([np.arange(t, min(t + 8, h)) for t in range(8 * f, h, 24)])
+            assert np.array_equal(part, full[rows]), f
+
+
+def test_streams_keep_separate_records(env):
+    """Two streams launching the same scene concurrently: each has its own
+    record, and more streams than the record holds run unscheduled."""
+    from rtclj import scenes
+    torch = env[2]
+    sc = env[0]
+    w, h = 240, 135
+    cam = scenes.cover_camera(w, h)
+    want = _render(sc, cam, w, h, 4)
+    streams = [torch.cuda.Stream() for _ in range(10)]
+    for _ in range(2):
+        for s in streams:
+            assert np.array_equal(_launch(env, cam, w, h, 4, stream=s), want)
+    # concurrent: enqueue on both streams before synchronising either
+    from rtclj._lib import check, lib, rt_params
+    _, ds, _ = env
+    p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=4, max_depth=50, seed=1)
+    outs = []
+    for s in streams[:2]:
+        with torch.cuda.stream(s):
+            o = torch.full((h * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        outs.append(o)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for s, o in zip(streams[:2], outs):
+            check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(o.data_ptr()), None,
+                                C.c_void_p(s.cuda_stream)))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().reshape(h, w, 3), want)
