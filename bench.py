@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4; big-body scan test = 16
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16d"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16e"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -333,7 +333,7 @@ def main():
             "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
-            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 4 lanes/pixel)" % a.variant,
+            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 4x4-pixel sample pool per wave)" % a.variant,
             "cpu_baseline": None,
         }
         if a.cpu_baseline == "auto" and world == 1:

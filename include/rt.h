@@ -206,8 +206,14 @@ int rt_set_variant(int variant);
  * fit): for reading the matching statistics build.  -1 on a NULL scene. */
 int rt_resolve_variant(const rt_dscene* ds);
 
-/* Lanes per pixel (1, 2, 4; 0 = automatic by frame size): how many lanes
- * share one pixel's four sample stripes.  Changes the launch shape, never the
+/* Launch shape.  1, 2, 4: lanes per pixel, each lane running a fixed share
+ * of the pixel's four sample stripes.  -1 / -2: the sample pool, a wave owns
+ * 4 x 4 / 8 x 8 pixels and every (pixel, sample) pair of them; a lane whose
+ * path ends takes the next pair, the colours go to a per-wave scratch and are
+ * summed per stripe in sample order after the pool (BVH variants 11, 13,
+ * 16-19; the scratch is per scene and stream, about 12 bytes per sample up to
+ * 2 GiB a launch, more launches beyond).  0 = automatic: the 4 x 4 pool where
+ * the variant has it, else by frame size.  Changes the launch shape, never the
  * result.  Returns the previous value. */
 int rt_set_lanes_per_pixel(int lpp);
 

@@ -32,6 +32,7 @@
 // See DESIGN.md §3.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -75,6 +76,9 @@ struct alignas(16) KArgs {
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
   unsigned* tile_cost;     // nullable: per tile, the longest of its waves' durations (s_memrealtime ticks)
+  float* pool_scratch;     // sample pool (LPP 0): per wave 16 pixels x pool_chunk samples x rgb
+  int pool_chunk;          // samples per pixel per pool round (one launch per round)
+  int pool_c0;             // this launch's round starts at sample pool_c0 of each pixel
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
@@ -167,7 +171,15 @@ __device__ __forceinline__ int stripe_begin(int s, int spp, int P) {
 
 template <int SRC, int SCAN, int LPP, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
-  static_assert(LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel");
+  static_assert(LPP == -2 || LPP == -1 || LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel (< 0: sample pool)");
+  // LPP -1 / -2 = the sample pool: a wave owns a 4 x 4 / 8 x 8 pixel tile and
+  // the tile's pixel x sample pairs; a lane whose path ends takes the next
+  // pair, so no lane idles until the pool is empty.  Each sample's colour goes
+  // to the wave's scratch; after the pool, lane (pixel, stripe) (4 x 4) or
+  // lane = pixel (8 x 8) adds the samples in sample order, stripe by stripe:
+  // the stripe contract of LPP 4 / 1, same bits.
+  constexpr bool POOL = LPP < 0;
+  constexpr int LPPE = LPP == -1 ? 4 : LPP == -2 ? 1 : LPP;
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
@@ -193,10 +205,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // lane -> (pixel, stripe group): a wave owns a TW x TH pixel tile
   // (PX = 64/LPP pixels), lane group grp = lane / PX; the block's 4 waves
   // tile 2 x 2.
-  constexpr int PX = 64 / LPP;
-  constexpr int TW = (LPP == 4) ? 4 : 8;
-  constexpr int TH = (LPP == 1) ? 8 : 4;
-  const int wave = threadIdx.x >> 6;
+  constexpr int PX = 64 / LPPE;
+  constexpr int TW = (LPPE == 4) ? 4 : 8;
+  constexpr int TH = (LPPE == 1) ? 8 : 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int lane = threadIdx.x & 63;
   const int pl = lane % PX;     // pixel within the wave tile
   const int grp = lane / PX;    // stripe group
@@ -204,34 +216,58 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int slot = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
   const int tile = a.tile_order ? a.tile_order[slot] : slot;
   const int tbx = tile % static_cast<int>(gridDim.x), tby = tile / static_cast<int>(gridDim.x);
-  const int px = tbx * (2 * TW) + (wave & 1) * TW + (pl % TW);
-  const int ro = tby * (2 * TH) + (wave >> 1) * TH + (pl / TW);
-  const bool in_image = (px < a.width) && (ro < a.rows_out);
+  const int x0 = tbx * (2 * TW) + (wave & 1) * TW;   // the wave's tile
+  const int y0 = tby * (2 * TH) + (wave >> 1) * TH;
+  // pool: the tile's in-image part, vw x vh pixels, pixel q at (q % vw, q / vw)
+  const int vw = POOL ? max(0, min(TW, a.width - x0)) : TW;
+  const int vh = POOL ? max(0, min(TH, a.rows_out - y0)) : TH;
+  const int npx = vw * vh;
+  int px = POOL ? x0 + (vw > 0 ? pl % vw : 0) : x0 + (pl % TW);
+  int ro = POOL ? y0 + (vw > 0 ? pl / vw : 0) : y0 + (pl / TW);
+  const bool in_image = POOL ? (pl < npx) : (px < a.width) && (ro < a.rows_out);
   bool active = in_image;
 
   // compacted output row -> global image row (interleaved row tiles)
-  int gy = a.row_begin + ro;
-  if (a.tile_step > 0) {
-    const int t = ro / a.row_tile;
-    gy = a.row_begin + (a.tile_first + t * a.tile_step) * a.row_tile + (ro - t * a.row_tile);
-  }
+  auto image_row = [&](int r) {
+    if (a.tile_step > 0) {
+      const int t = r / a.row_tile;
+      return a.row_begin + (a.tile_first + t * a.tile_step) * a.row_tile + (r - t * a.row_tile);
+    }
+    return a.row_begin + r;
+  };
+  auto pixel_key = [&](int x, int y) {
+    return mix32(a.key ^ mix32(static_cast<uint32_t>(y) * static_cast<uint32_t>(a.width) + static_cast<uint32_t>(x)));
+  };
+  int gy = image_row(ro);
 
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
-  const uint32_t pkey = mix32(a.key ^ mix32(static_cast<uint32_t>(gy) * static_cast<uint32_t>(a.width) +
-                                            static_cast<uint32_t>(px)));
+  uint32_t pkey = pixel_key(px, gy);
 
   // this lane's samples [k, k_end) = stripes [grp*SPL, (grp+1)*SPL)
   const int P = a.spp < 4 ? (a.spp > 0 ? a.spp : 1) : 4;
-  constexpr int SPL = 4 / LPP;  // stripes per lane (LPP > 1 requires P == 4)
-  int k = LPP == 1 ? 0 : stripe_begin(grp * SPL, a.spp, P);
-  const int k_end = LPP == 1 ? a.spp : stripe_begin(grp * SPL + SPL, a.spp, P);
-  int stripe = LPP == 1 ? 0 : grp * SPL;             // current stripe index
+  constexpr int SPL = 4 / LPPE;  // stripes per lane (LPP > 1 requires P == 4)
+  int k = LPPE == 1 ? 0 : stripe_begin(grp * SPL, a.spp, P);
+  const int k_end = LPPE == 1 ? a.spp : stripe_begin(grp * SPL + SPL, a.spp, P);
+  int stripe = LPPE == 1 ? 0 : grp * SPL;            // current stripe index
   int k_next = stripe_begin(stripe + 1, a.spp, P);   // its end
   float accr = 0.0f, accg = 0.0f, accb = 0.0f;       // current stripe sum
   float totr = 0.0f, totg = 0.0f, totb = 0.0f;       // LPP == 1: running total
   float s0r = 0.0f, s0g = 0.0f, s0b = 0.0f;          // LPP == 2: the lane's first stripe sum
   uint32_t segs = 0;
-  if (a.spp <= 0 || a.max_depth <= 0 || k >= k_end) active = false;  // depth<=0 -> black (:46-47)
+  if (!POOL && (a.spp <= 0 || a.max_depth <= 0 || k >= k_end)) active = false;  // depth<=0 -> black (:46-47)
+
+  // pool state: round [c0, c0 + cn) of each pixel's samples; pool index j ->
+  // (pixel j % npx, sample c0 + j / npx); the next free index is `base`
+  // the wave's scratch: PX pixels x pool_chunk samples x rgb, then the 64
+  // lanes' sums between rounds (total and current stripe, rgb each)
+  float* const scr = POOL ? a.pool_scratch + (static_cast<size_t>(tile) * 4 + wave) *
+                                                 (static_cast<size_t>(PX * 3) * a.pool_chunk + 64 * 6)
+                          : nullptr;
+  int c0 = 0, cn = 0, pool = 0, j = lane, base = 64, q = 0;
+  const bool pool_work = a.spp > 0 && a.max_depth > 0 && npx > 0;
+  // j / npx and q / vw by multiply-high (exact for j < 2^32 / 16)
+  const uint32_t mag_npx = npx > 0 ? 0xffffffffu / static_cast<uint32_t>(npx) + 1u : 0u;
+  const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
 
   // path state
   uint32_t st = 0;
@@ -241,6 +277,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   int last = -1;   // body the current ray leaves (-1: camera ray)
   bool fresh = true;
 
+  if constexpr (POOL) {   // this launch's round: samples [c0, c0 + cn) of every pixel
+    c0 = a.pool_c0;
+    cn = min(a.pool_chunk, a.spp - c0);
+    pool = pool_work ? npx * cn : 0;
+    active = j < pool;
+  }
   while (active) {
     if constexpr (STATS) st_ts = stamp();
     if constexpr (STATS) {  // counted once per wave event, by its first active lane
@@ -251,6 +293,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       }
     }
     if (fresh) {
+      if constexpr (POOL) {   // pool index -> (pixel, sample)
+        const int s = npx == 1 ? j : static_cast<int>(__umulhi(static_cast<uint32_t>(j), mag_npx));
+        q = j - s * npx;
+        k = c0 + s;
+        const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
+        px = x0 + (q - qy * vw);
+        ro = y0 + qy;
+        gy = image_row(ro);
+        pkey = pixel_key(px, gy);
+      }
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
       st = mix32(pkey + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
@@ -762,7 +814,22 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       st_c_shade += t - st_ts;
       st_ts = t;
     }
-    if (done) {
+    if (POOL) {
+      if (done) {
+        float* d = scr + ((k - c0) * PX + q) * 3;
+        d[0] = cr;
+        d[1] = cg;
+        d[2] = cb;
+      }
+      const uint64_t m = __ballot(done);
+      if (done) {
+        j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+        fresh = true;
+        if (j >= pool) active = false;
+      }
+      base += static_cast<int>(__popcll(m));
+    } else if (done) {
       accr += cr;
       accg += cg;
       accb += cb;
@@ -789,14 +856,60 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
     if constexpr (STATS) st_c_acc += stamp() - st_ts;
   }
+  if constexpr (POOL) {
+    // the round's samples, in sample order, into lane (pixel pl, stripe
+    // grp)'s stripe sum (the wave's own stores: a workgroup-scope fence
+    // orders them); between rounds (launches) the sums wait in scratch
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    float* const sums = scr + PX * 3 * a.pool_chunk + lane * 6;
+    if (pl < npx && pool_work) {
+      if (c0 > 0) {
+        accr = sums[0];
+        accg = sums[1];
+        accb = sums[2];
+        totr = sums[3];
+        totg = sums[4];
+        totb = sums[5];
+      }
+      // LPP 4 shape: lane group grp's stripe; LPP 1 shape: every stripe, the
+      // completed ones into the running total
+      for (int sp = (LPPE == 4 ? grp : 0); sp < (LPPE == 4 ? grp + 1 : P); ++sp) {
+        const int b = stripe_begin(sp, a.spp, P), e = stripe_begin(sp + 1, a.spp, P);
+        const int sb = max(b, c0), se = min(e, c0 + cn);
+        for (int s = sb; s < se; ++s) {
+          const float* d = scr + ((s - c0) * PX + pl) * 3;
+          accr += d[0];
+          accg += d[1];
+          accb += d[2];
+        }
+        if (LPPE == 1 && e > c0 && e <= c0 + cn) {   // stripe sp completes in this round
+          totr += accr;
+          totg += accg;
+          totb += accb;
+          accr = accg = accb = 0.0f;
+        }
+      }
+      if (c0 + cn < a.spp) {   // more rounds follow: keep the sums, no output yet
+        sums[0] = accr;
+        sums[1] = accg;
+        sums[2] = accb;
+        sums[3] = totr;
+        sums[4] = totg;
+        sums[5] = totb;
+      }
+    }
+    px = x0 + (vw > 0 ? pl % vw : 0);   // the fold lane's own pixel again
+    ro = y0 + (vw > 0 ? pl / vw : 0);
+  }
 
   // ---- per-pixel total ((s0 + s1) + s2) + s3, / spp (raytracing.clj:155) ----
   float outr, outg, outb;
-  if constexpr (LPP == 1) {
+  if constexpr (LPPE == 1) {
     outr = totr;
     outg = totg;
     outb = totb;
-  } else if constexpr (LPP == 2) {
+  } else if constexpr (LPPE == 2) {
     // group 0 holds s0 (s0*) and s1 (acc*); group 1 holds s2 (s0*) and s3 (acc*)
     const float s2r = __shfl(s0r, pl + PX), s2g = __shfl(s0g, pl + PX), s2b = __shfl(s0b, pl + PX);
     const float s3r = __shfl(accr, pl + PX), s3g = __shfl(accg, pl + PX), s3b = __shfl(accb, pl + PX);
@@ -812,7 +925,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     outg = ((accg + s1g) + s2g) + s3g;
     outb = ((accb + s1b) + s2b) + s3b;
   }
-  if (in_image && grp == 0) {
+  if (in_image && grp == 0 && (!POOL || a.pool_c0 + a.pool_chunk >= a.spp)) {
     const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
     float* o = a.out + (static_cast<size_t>(ro) * a.width + px) * 3;
     if (a.realm) {
@@ -873,6 +986,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     // one 64-bit atomic per wave: segments and samples of its 64 lanes
     uint32_t v = segs;
     uint32_t smp = (in_image && grp == 0 && a.max_depth > 0 && a.spp > 0) ? static_cast<uint32_t>(a.spp) : 0u;
+    if (POOL && a.pool_c0 + a.pool_chunk < a.spp) smp = 0;   // counted by the last round
     for (int off = 32; off > 0; off >>= 1) {
       v += __shfl_xor(v, off);
       smp += __shfl_xor(smp, off);
@@ -924,10 +1038,12 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
 //  18 BVH in LDS, 8-body leaves (four pairs)                 19 = 18 + stats
 //     (BVH variants fall back to 5 when the tree does not fit / is too deep)
 //   0 = default (16, or 18 when the 4-body tree's LDS image is large)
-// Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 for the grouped scans,
-// 0 = automatic (enough waves to keep the chip full to the end).
+// Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 = fixed sample stripes
+// per lane; -1 / -2 = the sample pool with 4 x 4 / 8 x 8 pixels per wave (BVH
+// variants 11, 13, 16-19); 0 = automatic (the 4 x 4 pool where the variant has
+// it, else enough waves to keep the chip full to the end).
 struct Variant {
-  const void* fn[3];   // LPP 1, 2, 4
+  const void* fn[5];   // LPP 1, 2, 4, sample pool 4 x 4 (LPP -1), sample pool 8 x 8 (LPP -2)
   bool lds;
   bool stats;
 };
@@ -938,7 +1054,7 @@ static int variant_tree(int v) { return v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 static const Variant& variant_table(int v) {
   static const Variant t[kVariants] = {
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
       {{RT_K(SRC_SCALAR, SCAN_SIMPLE, 1, false), nullptr, nullptr}, false, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, true), nullptr, nullptr}, true, true},
@@ -957,32 +1073,41 @@ static const Variant& variant_table(int v) {
       {{RT_K(SRC_SCALAR, SCAN_PK4, 1, true), RT_K(SRC_SCALAR, SCAN_PK4, 2, true),
         RT_K(SRC_SCALAR, SCAN_PK4, 4, true)}, false, true},
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false)}, true, false},
       {{RT_K(SRC_SCALAR, SCAN_BVH, 1, false), RT_K(SRC_SCALAR, SCAN_BVH, 2, false),
         RT_K(SRC_SCALAR, SCAN_BVH, 4, false)}, false, false},
       {{RT_K(SRC_LDS, SCAN_BVH, 1, true), RT_K(SRC_LDS, SCAN_BVH, 2, true),
-        RT_K(SRC_LDS, SCAN_BVH, 4, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVH, 4, true), RT_K(SRC_LDS, SCAN_BVH, -1, true), RT_K(SRC_LDS, SCAN_BVH, -2, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHWW, 1, false), RT_K(SRC_LDS, SCAN_BVHWW, 2, false),
         RT_K(SRC_LDS, SCAN_BVHWW, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHWW, 1, true), RT_K(SRC_LDS, SCAN_BVHWW, 2, true),
         RT_K(SRC_LDS, SCAN_BVHWW, 4, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHQ, 1, false), RT_K(SRC_LDS, SCAN_BVHQ, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, false), RT_K(SRC_LDS, SCAN_BVHQ, -1, false), RT_K(SRC_LDS, SCAN_BVHQ, -2, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHQ, 1, true), RT_K(SRC_LDS, SCAN_BVHQ, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, true), RT_K(SRC_LDS, SCAN_BVHQ, -1, true), RT_K(SRC_LDS, SCAN_BVHQ, -2, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHO, 1, false), RT_K(SRC_LDS, SCAN_BVHO, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVHO, 4, false), RT_K(SRC_LDS, SCAN_BVHO, -1, false), RT_K(SRC_LDS, SCAN_BVHO, -2, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHO, 1, true), RT_K(SRC_LDS, SCAN_BVHO, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVHO, 4, true), RT_K(SRC_LDS, SCAN_BVHO, -1, true), RT_K(SRC_LDS, SCAN_BVHO, -2, true)}, true, true},
   };
   return t[(v >= 0 && v < kVariants) ? v : 0];
 }
 #undef RT_K
-static int g_lpp = 0;  // 0 = automatic
+static int g_lpp = 0;  // 0 = automatic, -1 / -2 = sample pool 4 x 4 / 8 x 8
+// sample-pool scratch per launch (beyond it: more rounds); RTCLJ_POOL_BYTES
+// lowers it (tests: many rounds on a small frame)
+static size_t pool_bytes() {
+  const char* e = std::getenv("RTCLJ_POOL_BYTES");
+  const long long v = e ? std::atoll(e) : 0;
+  return v > 0 ? static_cast<size_t>(v) : (size_t(2) << 30);
+}
 
 // Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
 // last waves then drain quickly); 1 lane keeps the SIMD fuller per wave.
-static int choose_lpp(int width, int rows, int spp, bool have_all) {
+static int choose_lpp(int width, int rows, int spp, bool have_all, bool have_pool) {
+  if ((g_lpp == -1 || g_lpp == -2) && have_pool) return g_lpp;
+  if (g_lpp == 0 && have_pool) return -1;   // automatic: the 4 x 4 sample pool where the variant has it
   if (!have_all || spp < 4) return 1;
   if (g_lpp == 1 || g_lpp == 2 || g_lpp == 4) return g_lpp;
   const long long target = 48 * 1024;  // ~6 x the waves an MI355X keeps resident
@@ -1031,6 +1156,8 @@ struct Schedule {
   hipStream_t stream = nullptr;
   unsigned* cost = nullptr;
   int* order = nullptr;
+  float* scratch = nullptr;   // the sample pool's per-wave sample colours
+  size_t scratch_bytes = 0;
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
@@ -1044,6 +1171,7 @@ struct ScheduleSet {
     for (int k = 0; k < used; ++k) {
       if (s[k].cost) (void)hipFree(s[k].cost);
       if (s[k].order) (void)hipFree(s[k].order);
+      if (s[k].scratch) (void)hipFree(s[k].scratch);
     }
     used = 0;
   }
@@ -1087,7 +1215,7 @@ extern "C" int rt_set_schedule(int mode) {
 
 extern "C" int rt_set_lanes_per_pixel(int lpp) {
   const int old = g_lpp;
-  if (lpp == 0 || lpp == 1 || lpp == 2 || lpp == 4) g_lpp = lpp;
+  if (lpp == -2 || lpp == -1 || lpp == 0 || lpp == 1 || lpp == 2 || lpp == 4) g_lpp = lpp;
   return old;
 }
 
@@ -1275,12 +1403,28 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.bvh_stack = tr.depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
-  const int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr);
-  const int tw = lpp == 4 ? 4 : 8, th = lpp == 1 ? 8 : 4;   // wave tile (trace_kernel)
+  hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr, v.fn[3] != nullptr);
+  // per-stream state of this scene: the adaptive schedule's record and the
+  // sample pool's scratch (both only ever used by this stream's kernels)
+  Schedule* sch = nullptr;
+  std::unique_lock<std::mutex> sched_lock;
+  if (g_schedule == 0 || lpp < 0) {
+    ScheduleSet& set = ds->sched;
+    sched_lock = std::unique_lock<std::mutex>(set.mu);
+    for (int k = 0; k < set.used && !sch; ++k)
+      if (set.s[k].stream == stream) sch = &set.s[k];
+    if (!sch && set.used < kSchedStreams) {
+      sch = &set.s[set.used++];
+      sch->stream = stream;
+    }
+    if (!sch && lpp < 0) lpp = lpp == -1 && p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
+  }
+  const int tw = (lpp == 4 || lpp == -1) ? 4 : 8, th = (lpp == 1 || lpp == -2) ? 8 : 4;   // wave tile (trace_kernel)
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
   const dim3 block(256);
-  const void* fn = v.fn[lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
-  hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  const void* fn = v.fn[lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
+  const int n_tiles = static_cast<int>(grid.x * grid.y);
   if (v.stats) {
     if (!g_dbg) {
       HIP_TRY(hipMalloc(&g_dbg, 16 * sizeof(unsigned long long)));
@@ -1301,11 +1445,30 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     if (lds > 64 * 1024)
       HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   }
+  if (lpp < 0) {
+    // pool scratch: per wave 16 / 64 pixels x chunk samples x rgb, chunk = spp
+    // up to pool_bytes() for the whole launch (more rounds beyond that), + the
+    // 64 lanes' sums between rounds (6 floats)
+    const size_t waves = static_cast<size_t>(n_tiles) * 4;
+    const size_t per_sample = waves * (lpp == -1 ? 16 : 64) * 3 * sizeof(float);
+    const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(p->spp > 0 ? p->spp : 1,
+                                                                            pool_bytes() / per_sample)));
+    const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
+    if (sch->scratch_bytes < need) {   // grow (this stream's kernels may still use the old one)
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->scratch) (void)hipFree(sch->scratch);
+      sch->scratch = nullptr;
+      sch->scratch_bytes = 0;
+      HIP_TRY(hipMalloc(&sch->scratch, need));
+      sch->scratch_bytes = need;
+    }
+    a.pool_scratch = sch->scratch;
+    a.pool_chunk = chunk;
+  }
   // adaptive schedule: dispatch tiles longest first, by the durations the
-  // previous launch of this frame geometry on this scene and stream measured
-  Schedule* sch = nullptr;
-  std::unique_lock<std::mutex> sched_lock;
-  if (g_schedule == 0) {
+  // previous launch of this launch shape on this scene and stream measured
+  bool scheduled = false;
+  if (g_schedule == 0 && sch) {
     ScheduleKey key{};
     key.width = a.width;
     key.rows = a.rows_out;
@@ -1317,20 +1480,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     key.lpp = lpp;
     key.gx = static_cast<int>(grid.x);
     key.gy = static_cast<int>(grid.y);
-    const int n_tiles = key.gx * key.gy;
-    ScheduleSet& set = ds->sched;
-    sched_lock = std::unique_lock<std::mutex>(set.mu);
-    for (int k = 0; k < set.used && !sch; ++k)
-      if (set.s[k].stream == stream) sch = &set.s[k];
-    if (!sch && set.used < kSchedStreams) {
-      sch = &set.s[set.used++];
-      sch->stream = stream;
-    }
-    if (sch && std::memcmp(&sch->key, &key, sizeof key) != 0) {
+    if (std::memcmp(&sch->key, &key, sizeof key) != 0) {
       sch->ready = false;
       sch->key = key;
     }
-    if (sch && sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
+    if (sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
       HIP_TRY(hipStreamSynchronize(stream));
       if (sch->cost) (void)hipFree(sch->cost);
       if (sch->order) (void)hipFree(sch->order);
@@ -1342,19 +1496,25 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMalloc(&sch->order, n_tiles * sizeof(int)));
       sch->cap = n_tiles;
     }
-    if (sch) {
-      if (sch->ready) a.tile_order = sch->order;
-      a.tile_cost = sch->cost;
-      HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
-    }
+    if (sch->ready) a.tile_order = sch->order;
+    a.tile_cost = sch->cost;
+    HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
+    scheduled = true;
   }
   void* args[] = {&a};
-  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
-  if (sch) {
+  if (lpp < 0) {   // the sample pool: one launch per round of pool_chunk samples per pixel
+    for (a.pool_c0 = 0;; a.pool_c0 += a.pool_chunk) {
+      HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
+      if (a.pool_c0 + a.pool_chunk >= p->spp) break;
+    }
+  } else {
+    HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
+  }
+  if (scheduled) {
     // the next launch's order, stream-ordered after this kernel (no host sync)
     const unsigned* cost = sch->cost;
     int* order = sch->order;
-    int n = static_cast<int>(grid.x * grid.y);
+    int n = n_tiles;
     void* sargs[] = {&cost, &order, &n};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
     sch->ready = true;
