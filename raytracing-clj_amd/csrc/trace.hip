@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if (!POOL && (a.spp <= 0 || a.max_depth <= 0 || k >= k_end)) active = false;  // depth<=0 -> black (:46-47)
 
   // pool state: round [c0, c0 + cn) of each pixel's samples; pool index j ->
-  // (pixel j % npx, sample c0 + j / npx); the next free index is `base`
+  // (pixel j / cn, sample c0 + j % cn); the next free index is `base`
   // the wave's scratch: PX pixels x pool_chunk samples x rgb, then the 64
   // lanes' sums between rounds (total and current stripe, rgb each)
   float* const scr = POOL ? a.pool_scratch + (static_cast<size_t>(tile) * 4 + wave) *
@@ -265,9 +265,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
                           : nullptr;
   int c0 = 0, cn = 0, pool = 0, j = lane, base = 64, q = 0;
   const bool pool_work = a.spp > 0 && a.max_depth > 0 && npx > 0;
-  // j / npx and q / vw by multiply-high (exact for j < 2^32 / 16)
-  const uint32_t mag_npx = npx > 0 ? 0xffffffffu / static_cast<uint32_t>(npx) + 1u : 0u;
+  // j / cn and q / vw by multiply-high: exact while j * cn < 2^32, i.e.
+  // 16 * cn^2 < 2^32 (the host caps cn at 16384); divisor 1 is special-cased
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
+  uint32_t mag_cn = 0;
 
   // path state
   uint32_t st = 0;
@@ -281,6 +282,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     c0 = a.pool_c0;
     cn = min(a.pool_chunk, a.spp - c0);
     pool = pool_work ? npx * cn : 0;
+    mag_cn = cn > 0 ? 0xffffffffu / static_cast<uint32_t>(cn) + 1u : 0u;
     active = j < pool;
   }
   while (active) {
@@ -294,9 +296,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
     if (fresh) {
       if constexpr (POOL) {   // pool index -> (pixel, sample)
-        const int s = npx == 1 ? j : static_cast<int>(__umulhi(static_cast<uint32_t>(j), mag_npx));
-        q = j - s * npx;
-        k = c0 + s;
+        // pixel-major: the lanes in flight hold consecutive samples of one or
+        // two pixels (the most coherent rays; 1-2 % faster than pixel-minor)
+        q = cn == 1 ? j : static_cast<int>(__umulhi(static_cast<uint32_t>(j), mag_cn));
+        k = c0 + (j - q * cn);
         const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
         px = x0 + (q - qy * vw);
         ro = y0 + qy;
@@ -1451,8 +1454,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // 64 lanes' sums between rounds (6 floats)
     const size_t waves = static_cast<size_t>(n_tiles) * 4;
     const size_t per_sample = waves * (lpp == -1 ? 16 : 64) * 3 * sizeof(float);
-    const int chunk = static_cast<int>(std::max<size_t>(1, std::min<size_t>(p->spp > 0 ? p->spp : 1,
-                                                                            pool_bytes() / per_sample)));
+    const int chunk = static_cast<int>(std::max<size_t>(
+        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), pool_bytes() / per_sample, 16384})));
     const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
     if (sch->scratch_bytes < need) {   // grow (this stream's kernels may still use the old one)
       HIP_TRY(hipStreamSynchronize(stream));
@@ -1463,6 +1466,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch->scratch_bytes = need;
     }
     a.pool_scratch = sch->scratch;
+
     a.pool_chunk = chunk;
   }
   // adaptive schedule: dispatch tiles longest first, by the durations the
