@@ -209,11 +209,12 @@ int rt_resolve_variant(const rt_dscene* ds);
 /* Launch shape.  1, 2, 4: lanes per pixel, each lane running a fixed share
  * of the pixel's four sample stripes.  -1 / -2: the sample pool, a wave owns
  * 4 x 4 / 8 x 8 pixels and every (pixel, sample) pair of them; a lane whose
- * path ends takes the next pair, the colours go to a per-wave scratch and are
- * summed per stripe in sample order after the pool (BVH variants 11, 13,
- * 16-19; the scratch is per scene and stream, about 12 bytes per sample up to
- * 2 GiB a launch, more launches beyond).  0 = automatic: the 4 x 4 pool where
- * the variant has it, else by frame size.  Changes the launch shape, never the
+ * path ends takes the next pair, the colours go to a scratch and are summed
+ * per stripe in sample order after the pool.  -3: one pool of 8 x 8 pixels
+ * per workgroup, shared by its 4 waves.  Pools exist for the BVH variants 11,
+ * 13, 16-19; the scratch is per scene and stream, about 12 bytes per sample
+ * up to 2 GiB a launch, more launches beyond.  0 = automatic: -3 where the
+ * variant has it, else by frame size.  Changes the launch shape, never the
  * result.  Returns the previous value. */
 int rt_set_lanes_per_pixel(int lpp);
 
@@ -221,8 +222,8 @@ int rt_set_lanes_per_pixel(int lpp);
  * records how long each tile's waves ran, and a one-block sort enqueued after
  * it (same stream, no host sync) turns that into a longest-first order; the
  * next launch on the same scene and stream with the same launch shape (width,
- * row selection, kernel variant, lanes per pixel; camera, spp, seed and flags
- * may differ) dispatches its tiles in that order, so the slow tiles do not
+ * row selection, lanes per pixel; camera, spp, seed, flags and the kernel
+ * variant may differ) dispatches its tiles in that order, so the slow tiles do not
  * trail the kernel's end.  A launch of another shape runs in plain order and
  * re-keys the record (per scene, up to 8 streams; launches on further streams
  * are unscheduled).  1 = always plain order.  Changes timing only: every

@@ -171,15 +171,23 @@ __device__ __forceinline__ int stripe_begin(int s, int spp, int P) {
 
 template <int SRC, int SCAN, int LPP, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
-  static_assert(LPP == -2 || LPP == -1 || LPP == 1 || LPP == 2 || LPP == 4, "lanes per pixel (< 0: sample pool)");
+  static_assert(LPP == -3 || LPP == -2 || LPP == -1 || LPP == 1 || LPP == 2 || LPP == 4,
+                "lanes per pixel (< 0: sample pool)");
   // LPP -1 / -2 = the sample pool: a wave owns a 4 x 4 / 8 x 8 pixel tile and
   // the tile's pixel x sample pairs; a lane whose path ends takes the next
   // pair, so no lane idles until the pool is empty.  Each sample's colour goes
   // to the wave's scratch; after the pool, lane (pixel, stripe) (4 x 4) or
   // lane = pixel (8 x 8) adds the samples in sample order, stripe by stripe:
-  // the stripe contract of LPP 4 / 1, same bits.
+  // the stripe contract of LPP 4 / 1, same bits.  LPP -3: one pool per
+  // workgroup, its 8 x 8 pixels shared by the 4 waves (refills through an LDS
+  // counter), so the waves of a workgroup finish together; each wave sums 16
+  // of the pixels as LPP -1 does.
   constexpr bool POOL = LPP < 0;
-  constexpr int LPPE = LPP == -1 ? 4 : LPP == -2 ? 1 : LPP;
+  constexpr bool WGP = LPP == -3;
+  constexpr int LPPE = (LPP == -1 || LPP == -3) ? 4 : LPP == -2 ? 1 : LPP;
+  constexpr int PPX = (LPP == -2 || LPP == -3) ? 64 : 16;   // pixels of one pool
+  static_assert(!WGP || (SRC == SRC_LDS && is_bvh_scan(SCAN)), "workgroup pool: LDS BVH variants");
+  __shared__ int s_pool_next;   // WGP: the workgroup pool's next free index
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
@@ -190,6 +198,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int n = a.n;
   if constexpr (is_bvh_scan(SCAN)) {
     if constexpr (SRC == SRC_LDS) {
+      if (WGP && threadIdx.x == 0) s_pool_next = 256;   // (published by the barrier below)
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
       __syncthreads();
     }
@@ -218,13 +227,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int tbx = tile % static_cast<int>(gridDim.x), tby = tile / static_cast<int>(gridDim.x);
   const int x0 = tbx * (2 * TW) + (wave & 1) * TW;   // the wave's tile
   const int y0 = tby * (2 * TH) + (wave >> 1) * TH;
-  // pool: the tile's in-image part, vw x vh pixels, pixel q at (q % vw, q / vw)
-  const int vw = POOL ? max(0, min(TW, a.width - x0)) : TW;
-  const int vh = POOL ? max(0, min(TH, a.rows_out - y0)) : TH;
+  // pool: the pool tile's in-image part, vw x vh pixels, pixel q at
+  // (q % vw, q / vw); the pool tile is the wave's, or (WGP) the workgroup's
+  const int qx0 = WGP ? tbx * 8 : x0, qy0 = WGP ? tby * 8 : y0;
+  const int vw = POOL ? max(0, min(WGP ? 8 : TW, a.width - qx0)) : TW;
+  const int vh = POOL ? max(0, min(WGP ? 8 : TH, a.rows_out - qy0)) : TH;
   const int npx = vw * vh;
-  int px = POOL ? x0 + (vw > 0 ? pl % vw : 0) : x0 + (pl % TW);
-  int ro = POOL ? y0 + (vw > 0 ? pl / vw : 0) : y0 + (pl / TW);
-  const bool in_image = POOL ? (pl < npx) : (px < a.width) && (ro < a.rows_out);
+  const int fp = WGP ? wave * 16 + pl : pl;   // the pool pixel this lane sums (and writes)
+  int px = POOL ? qx0 + (vw > 0 ? fp % vw : 0) : x0 + (pl % TW);
+  int ro = POOL ? qy0 + (vw > 0 ? fp / vw : 0) : y0 + (pl / TW);
+  const bool in_image = POOL ? (fp < npx) : (px < a.width) && (ro < a.rows_out);
   bool active = in_image;
 
   // compacted output row -> global image row (interleaved row tiles)
@@ -258,12 +270,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 
   // pool state: round [c0, c0 + cn) of each pixel's samples; pool index j ->
   // (pixel j / cn, sample c0 + j % cn); the next free index is `base`
-  // the wave's scratch: PX pixels x pool_chunk samples x rgb, then the 64
+  // the pool's scratch: PPX pixels x pool_chunk samples x rgb, then the
   // lanes' sums between rounds (total and current stripe, rgb each)
-  float* const scr = POOL ? a.pool_scratch + (static_cast<size_t>(tile) * 4 + wave) *
-                                                 (static_cast<size_t>(PX * 3) * a.pool_chunk + 64 * 6)
+  float* const scr = POOL ? a.pool_scratch + (WGP ? static_cast<size_t>(tile) : static_cast<size_t>(tile) * 4 + wave) *
+                                                 (static_cast<size_t>(PPX * 3) * a.pool_chunk + (WGP ? 256 : 64) * 6)
                           : nullptr;
-  int c0 = 0, cn = 0, pool = 0, j = lane, base = 64, q = 0;
+  int c0 = 0, cn = 0, pool = 0, j = WGP ? static_cast<int>(threadIdx.x) : lane, base = 64, q = 0;
   const bool pool_work = a.spp > 0 && a.max_depth > 0 && npx > 0;
   // j / cn and q / vw by multiply-high: exact while j * cn < 2^32, i.e.
   // 16 * cn^2 < 2^32 (the host caps cn at 16384); divisor 1 is special-cased
@@ -301,8 +313,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         q = cn == 1 ? j : static_cast<int>(__umulhi(static_cast<uint32_t>(j), mag_cn));
         k = c0 + (j - q * cn);
         const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
-        px = x0 + (q - qy * vw);
-        ro = y0 + qy;
+        px = qx0 + (q - qy * vw);
+        ro = qy0 + qy;
         gy = image_row(ro);
         pkey = pixel_key(px, gy);
       }
@@ -505,7 +517,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // (the near plane's t is the min of the two planes' t, bit for bit: the
       // same fma on the same operands -- no min/max orders them)
       auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
-        const char* nb = reinterpret_cast<const char*>(nodes + node);
+        // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
+        const char* nb = reinterpret_cast<const char*>(nodes) + __umul24(static_cast<unsigned>(node), 80u);
         const f2* ax = reinterpret_cast<const f2*>(nb + offx);
         const f2* ay = reinterpret_cast<const f2*>(nb + offy);
         const f2* az = reinterpret_cast<const f2*>(nb + offz);
@@ -819,19 +832,27 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
     if (POOL) {
       if (done) {
-        float* d = scr + ((k - c0) * PX + q) * 3;
+        float* d = scr + ((k - c0) * PPX + q) * 3;
         d[0] = cr;
         d[1] = cg;
         d[2] = cb;
       }
       const uint64_t m = __ballot(done);
+      if constexpr (WGP) {   // one LDS atomic per wave event: the next popc(m) indices
+        if (m) {
+          const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
+          int old = 0;
+          if (lane == leader) old = atomicAdd(&s_pool_next, static_cast<int>(__popcll(m)));
+          base = __builtin_amdgcn_readlane(old, leader);
+        }
+      }
       if (done) {
         j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
         fresh = true;
         if (j >= pool) active = false;
       }
-      base += static_cast<int>(__popcll(m));
+      if constexpr (!WGP) base += static_cast<int>(__popcll(m));
     } else if (done) {
       accr += cr;
       accg += cg;
@@ -864,9 +885,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     // grp)'s stripe sum (the wave's own stores: a workgroup-scope fence
     // orders them); between rounds (launches) the sums wait in scratch
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if constexpr (WGP) __syncthreads();   // the other waves' samples too
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    float* const sums = scr + PX * 3 * a.pool_chunk + lane * 6;
-    if (pl < npx && pool_work) {
+    float* const sums = scr + PPX * 3 * a.pool_chunk + (WGP ? static_cast<int>(threadIdx.x) : lane) * 6;
+    if (fp < npx && pool_work) {
       if (c0 > 0) {
         accr = sums[0];
         accg = sums[1];
@@ -881,7 +903,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const int b = stripe_begin(sp, a.spp, P), e = stripe_begin(sp + 1, a.spp, P);
         const int sb = max(b, c0), se = min(e, c0 + cn);
         for (int s = sb; s < se; ++s) {
-          const float* d = scr + ((s - c0) * PX + pl) * 3;
+          const float* d = scr + ((s - c0) * PPX + fp) * 3;
           accr += d[0];
           accg += d[1];
           accb += d[2];
@@ -902,8 +924,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         sums[5] = totb;
       }
     }
-    px = x0 + (vw > 0 ? pl % vw : 0);   // the fold lane's own pixel again
-    ro = y0 + (vw > 0 ? pl / vw : 0);
+    px = qx0 + (vw > 0 ? fp % vw : 0);   // the fold lane's own pixel again
+    ro = qy0 + (vw > 0 ? fp / vw : 0);
   }
 
   // ---- per-pixel total ((s0 + s1) + s2) + s3, / spp (raytracing.clj:155) ----
@@ -1042,11 +1064,12 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
 //     (BVH variants fall back to 5 when the tree does not fit / is too deep)
 //   0 = default (16, or 18 when the 4-body tree's LDS image is large)
 // Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 = fixed sample stripes
-// per lane; -1 / -2 = the sample pool with 4 x 4 / 8 x 8 pixels per wave (BVH
-// variants 11, 13, 16-19); 0 = automatic (the 4 x 4 pool where the variant has
-// it, else enough waves to keep the chip full to the end).
+// per lane; -1 / -2 = the sample pool with 4 x 4 / 8 x 8 pixels per wave, -3 =
+// one pool of 8 x 8 pixels per workgroup (BVH variants 11, 13, 16-19); 0 =
+// automatic (-3 where the variant has it, else enough waves to keep the chip
+// full to the end).
 struct Variant {
-  const void* fn[5];   // LPP 1, 2, 4, sample pool 4 x 4 (LPP -1), sample pool 8 x 8 (LPP -2)
+  const void* fn[6];   // LPP 1, 2, 4, sample pool 4 x 4 (LPP -1), 8 x 8 (-2), workgroup 8 x 8 (-3)
   bool lds;
   bool stats;
 };
@@ -1057,7 +1080,7 @@ static int variant_tree(int v) { return v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 static const Variant& variant_table(int v) {
   static const Variant t[kVariants] = {
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false), RT_K(SRC_LDS, SCAN_BVH, -3, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
       {{RT_K(SRC_SCALAR, SCAN_SIMPLE, 1, false), nullptr, nullptr}, false, false},
       {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, true), nullptr, nullptr}, true, true},
@@ -1076,23 +1099,23 @@ static const Variant& variant_table(int v) {
       {{RT_K(SRC_SCALAR, SCAN_PK4, 1, true), RT_K(SRC_SCALAR, SCAN_PK4, 2, true),
         RT_K(SRC_SCALAR, SCAN_PK4, 4, true)}, false, true},
       {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false), RT_K(SRC_LDS, SCAN_BVH, -3, false)}, true, false},
       {{RT_K(SRC_SCALAR, SCAN_BVH, 1, false), RT_K(SRC_SCALAR, SCAN_BVH, 2, false),
         RT_K(SRC_SCALAR, SCAN_BVH, 4, false)}, false, false},
       {{RT_K(SRC_LDS, SCAN_BVH, 1, true), RT_K(SRC_LDS, SCAN_BVH, 2, true),
-        RT_K(SRC_LDS, SCAN_BVH, 4, true), RT_K(SRC_LDS, SCAN_BVH, -1, true), RT_K(SRC_LDS, SCAN_BVH, -2, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVH, 4, true), RT_K(SRC_LDS, SCAN_BVH, -1, true), RT_K(SRC_LDS, SCAN_BVH, -2, true), RT_K(SRC_LDS, SCAN_BVH, -3, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHWW, 1, false), RT_K(SRC_LDS, SCAN_BVHWW, 2, false),
         RT_K(SRC_LDS, SCAN_BVHWW, 4, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHWW, 1, true), RT_K(SRC_LDS, SCAN_BVHWW, 2, true),
         RT_K(SRC_LDS, SCAN_BVHWW, 4, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHQ, 1, false), RT_K(SRC_LDS, SCAN_BVHQ, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, false), RT_K(SRC_LDS, SCAN_BVHQ, -1, false), RT_K(SRC_LDS, SCAN_BVHQ, -2, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, false), RT_K(SRC_LDS, SCAN_BVHQ, -1, false), RT_K(SRC_LDS, SCAN_BVHQ, -2, false), RT_K(SRC_LDS, SCAN_BVHQ, -3, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHQ, 1, true), RT_K(SRC_LDS, SCAN_BVHQ, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, true), RT_K(SRC_LDS, SCAN_BVHQ, -1, true), RT_K(SRC_LDS, SCAN_BVHQ, -2, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVHQ, 4, true), RT_K(SRC_LDS, SCAN_BVHQ, -1, true), RT_K(SRC_LDS, SCAN_BVHQ, -2, true), RT_K(SRC_LDS, SCAN_BVHQ, -3, true)}, true, true},
       {{RT_K(SRC_LDS, SCAN_BVHO, 1, false), RT_K(SRC_LDS, SCAN_BVHO, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, false), RT_K(SRC_LDS, SCAN_BVHO, -1, false), RT_K(SRC_LDS, SCAN_BVHO, -2, false)}, true, false},
+        RT_K(SRC_LDS, SCAN_BVHO, 4, false), RT_K(SRC_LDS, SCAN_BVHO, -1, false), RT_K(SRC_LDS, SCAN_BVHO, -2, false), RT_K(SRC_LDS, SCAN_BVHO, -3, false)}, true, false},
       {{RT_K(SRC_LDS, SCAN_BVHO, 1, true), RT_K(SRC_LDS, SCAN_BVHO, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, true), RT_K(SRC_LDS, SCAN_BVHO, -1, true), RT_K(SRC_LDS, SCAN_BVHO, -2, true)}, true, true},
+        RT_K(SRC_LDS, SCAN_BVHO, 4, true), RT_K(SRC_LDS, SCAN_BVHO, -1, true), RT_K(SRC_LDS, SCAN_BVHO, -2, true), RT_K(SRC_LDS, SCAN_BVHO, -3, true)}, true, true},
   };
   return t[(v >= 0 && v < kVariants) ? v : 0];
 }
@@ -1109,8 +1132,8 @@ static size_t pool_bytes() {
 // Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
 // last waves then drain quickly); 1 lane keeps the SIMD fuller per wave.
 static int choose_lpp(int width, int rows, int spp, bool have_all, bool have_pool) {
-  if ((g_lpp == -1 || g_lpp == -2) && have_pool) return g_lpp;
-  if (g_lpp == 0 && have_pool) return -1;   // automatic: the 4 x 4 sample pool where the variant has it
+  if ((g_lpp == -1 || g_lpp == -2 || g_lpp == -3) && have_pool) return g_lpp;
+  if (g_lpp == 0 && have_pool) return -3;   // automatic: the workgroup sample pool where the variant has it
   if (!have_all || spp < 4) return 1;
   if (g_lpp == 1 || g_lpp == 2 || g_lpp == 4) return g_lpp;
   const long long target = 48 * 1024;  // ~6 x the waves an MI355X keeps resident
@@ -1145,15 +1168,15 @@ struct DTree {
 
 // Adaptive tile schedule (rt_launch): per stream, the per-tile durations of
 // the stream's last launch and the longest-first order derived from them, for
-// the launch shape `key` (frame rows, tiling, kernel variant, grid).  The
-// order is a prediction: camera, spp, seed and flags may change between
-// launches of one shape (progressive passes, animation) and it stays a good
-// one, and it never affects the result.  A launch of another shape re-keys the
+// the launch shape `key` (frame rows, tiling, lanes per pixel, grid).  The
+// order is a prediction: camera, spp, seed, flags and the kernel variant may
+// change between launches of one shape (progressive passes, animation, A/B)
+// and it stays a good one, and it never affects the result.  A launch of another shape re-keys the
 // entry (and runs in dispatch order once).  Entries are per stream so that nothing a
 // stream's kernels read is written from another stream; a dscene serves up to
 // kSchedStreams streams this way, launches on further streams run unscheduled.
 struct ScheduleKey {
-  int width, rows, row_begin, row_tile, tile_first, tile_step, variant, lpp, gx, gy;
+  int width, rows, row_begin, row_tile, tile_first, tile_step, lpp, gx, gy;
 };
 struct Schedule {
   hipStream_t stream = nullptr;
@@ -1218,7 +1241,7 @@ extern "C" int rt_set_schedule(int mode) {
 
 extern "C" int rt_set_lanes_per_pixel(int lpp) {
   const int old = g_lpp;
-  if (lpp == -2 || lpp == -1 || lpp == 0 || lpp == 1 || lpp == 2 || lpp == 4) g_lpp = lpp;
+  if (lpp >= -3 && lpp <= 4 && lpp != 3) g_lpp = lpp;
   return old;
 }
 
@@ -1421,12 +1444,12 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch = &set.s[set.used++];
       sch->stream = stream;
     }
-    if (!sch && lpp < 0) lpp = lpp == -1 && p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
+    if (!sch && lpp < 0) lpp = lpp != -2 && p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
   }
-  const int tw = (lpp == 4 || lpp == -1) ? 4 : 8, th = (lpp == 1 || lpp == -2) ? 8 : 4;   // wave tile (trace_kernel)
+  const int tw = (lpp == 4 || lpp == -1 || lpp == -3) ? 4 : 8, th = (lpp == 1 || lpp == -2) ? 8 : 4;   // wave tile
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
   const dim3 block(256);
-  const void* fn = v.fn[lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
+  const void* fn = v.fn[lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == -3 ? 5 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
   const int n_tiles = static_cast<int>(grid.x * grid.y);
   if (v.stats) {
     if (!g_dbg) {
@@ -1453,7 +1476,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // up to pool_bytes() for the whole launch (more rounds beyond that), + the
     // 64 lanes' sums between rounds (6 floats)
     const size_t waves = static_cast<size_t>(n_tiles) * 4;
-    const size_t per_sample = waves * (lpp == -1 ? 16 : 64) * 3 * sizeof(float);
+    const size_t per_sample = waves * (lpp == -2 ? 64 : 16) * 3 * sizeof(float);   // (-3: 64 per 4 waves)
     const int chunk = static_cast<int>(std::max<size_t>(
         1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), pool_bytes() / per_sample, 16384})));
     const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
@@ -1480,7 +1503,6 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     key.row_tile = a.row_tile;
     key.tile_first = a.tile_first;
     key.tile_step = a.tile_step;
-    key.variant = vsel;
     key.lpp = lpp;
     key.gx = static_cast<int>(grid.x);
     key.gy = static_cast<int>(grid.y);

@@ -162,7 +162,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
 
 
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
-@pytest.mark.parametrize("lpp", [1, 2, 4, -1, -2])
+@pytest.mark.parametrize("lpp", [1, 2, 4, -1, -2, -3])
 def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
     """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
     stats builds) and lanes-per-pixel launch shapes all give the mirror's bits."""
@@ -195,7 +195,7 @@ def test_sample_stripes_edge_spp(gpu_lib, spp):
     sc = _ref_scene()
     cam = R.camera(40, 22, **R.REFERENCE_CAMERA)
     ref, _, _ = _mirror(sc, cam, 40, 22, spp, 20, seed=8)
-    for lpp in (0, 1, 2, 4, -1, -2):
+    for lpp in (0, 1, 2, 4, -1, -2, -3):
         old = lib.rt_set_lanes_per_pixel(lpp)
         try:
             g = R.render(sc, cam, 40, 22, spp=spp, max_depth=20, seed=8)

@@ -49,7 +49,7 @@ def _render(sc, cam, w, h, spp, **kw):
     return R.render(sc, cam, w, h, spp=spp, max_depth=50, **kw)
 
 
-@pytest.mark.parametrize("variant,lpp", [(0, 0), (0, 1), (0, 4), (11, 0), (18, 2), (5, 0), (0, -1), (18, -1), (0, -2), (11, -2)])
+@pytest.mark.parametrize("variant,lpp", [(0, 0), (0, 1), (0, 4), (11, 0), (18, 2), (5, 0), (0, -1), (18, -1), (0, -2), (11, -2), (0, -3), (18, -3)])
 def test_repeated_launches_are_bit_identical(env, variant, lpp):
     from rtclj import scenes
     from rtclj._lib import lib
@@ -148,11 +148,11 @@ def test_streams_keep_separate_records(env):
         assert np.array_equal(o.cpu().numpy().reshape(h, w, 3), want)
 
 
-@pytest.mark.parametrize("lpp", [-1, -2])
+@pytest.mark.parametrize("lpp", [-1, -2, -3])
 @pytest.mark.parametrize("spp,pool_bytes", [(10, 3), (7, 1), (9, 4), (1, 0), (3, 0)])
 def test_sample_pool_rounds(env, monkeypatch, spp, pool_bytes, lpp):
-    """The sample pools (rt_set_lanes_per_pixel(-1 / -2): 4x4 / 8x8 pixels per
-    wave) in several rounds (scratch limited through RTCLJ_POOL_BYTES to
+    """The sample pools (rt_set_lanes_per_pixel(-1 / -2 / -3): 4x4 / 8x8 pixels
+    per wave, 8x8 per workgroup) in several rounds (scratch limited through RTCLJ_POOL_BYTES to
     `pool_bytes` samples per pixel; 9 spp in rounds of 4 ends stripes inside
     and at round ends), and with spp < 4: the stripe contract's bits, via
     rt_launch and rt_render."""
@@ -162,10 +162,10 @@ def test_sample_pool_rounds(env, monkeypatch, spp, pool_bytes, lpp):
     w, h = 150, 77
     cam = scenes.cover_camera(w, h)
     want = _render(sc, cam, w, h, spp)             # default launch shape (stripes)
-    t = 8 if lpp == -1 else 16
+    t = 16 if lpp == -2 else 8
     tiles = ((w + t - 1) // t) * ((h + t - 1) // t)
     if pool_bytes:
-        monkeypatch.setenv("RTCLJ_POOL_BYTES", str(tiles * 4 * (16 if lpp == -1 else 64) * 12 * pool_bytes))
+        monkeypatch.setenv("RTCLJ_POOL_BYTES", str(tiles * 4 * (64 if lpp == -2 else 16) * 12 * pool_bytes))
     old = lib.rt_set_lanes_per_pixel(lpp)
     try:
         for _ in range(2):
