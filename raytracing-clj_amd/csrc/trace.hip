@@ -1131,16 +1131,17 @@ static size_t pool_bytes() {
 
 // Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
 // last waves then drain quickly); 1 lane keeps the SIMD fuller per wave.
-static int choose_lpp(int width, int rows, int spp, bool have_all, bool have_pool) {
-  if ((g_lpp == -1 || g_lpp == -2 || g_lpp == -3) && have_pool) return g_lpp;
-  if (g_lpp == 0 && have_pool) return -3;   // automatic: the workgroup sample pool where the variant has it
-  if (!have_all || spp < 4) return 1;
-  if (g_lpp == 1 || g_lpp == 2 || g_lpp == 4) return g_lpp;
+static int fn_slot(int lpp) { return lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == -3 ? 5 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2; }
+static int choose_lpp(int width, int rows, int spp, const Variant& v) {
+  const auto has = [&](int lpp) { return v.fn[fn_slot(lpp)] != nullptr && (lpp < 0 || lpp == 1 || spp >= 4); };
+  if (g_lpp != 0 && has(g_lpp)) return g_lpp;
+  if (has(-3)) return -3;   // automatic: the workgroup sample pool where the variant has it
+  if (!v.fn[2] || spp < 4) return v.fn[0] ? 1 : -3;
   const long long target = 48 * 1024;  // ~6 x the waves an MI355X keeps resident
   const long long w1 = 4LL * ((width + 15) / 16) * ((rows + 15) / 16);
   const long long w2 = 4LL * ((width + 15) / 16) * ((rows + 7) / 8);
-  if (w1 >= target) return 1;
-  if (w2 >= target) return 2;
+  if (w1 >= target && v.fn[0]) return 1;
+  if (w2 >= target && v.fn[1]) return 2;
   return 4;
 }
 static int g_variant = 0;
@@ -1430,7 +1431,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  int lpp = choose_lpp(p->width, rows, p->spp, v.fn[2] != nullptr, v.fn[3] != nullptr);
+  int lpp = choose_lpp(p->width, rows, p->spp, v);
   // per-stream state of this scene: the adaptive schedule's record and the
   // sample pool's scratch (both only ever used by this stream's kernels)
   Schedule* sch = nullptr;
@@ -1444,12 +1445,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch = &set.s[set.used++];
       sch->stream = stream;
     }
-    if (!sch && lpp < 0) lpp = lpp != -2 && p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
+    if (!sch && lpp < 0) lpp = p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
   }
   const int tw = (lpp == 4 || lpp == -1 || lpp == -3) ? 4 : 8, th = (lpp == 1 || lpp == -2) ? 8 : 4;   // wave tile
   const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
   const dim3 block(256);
-  const void* fn = v.fn[lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == -3 ? 5 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2];
+  const void* fn = v.fn[fn_slot(lpp)];
+  if (!fn) return set_error(RT_E_ARG, "rt_launch: kernel variant " + std::to_string(vsel) + " has no launch shape for this frame");
   const int n_tiles = static_cast<int>(grid.x * grid.y);
   if (v.stats) {
     if (!g_dbg) {
