@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4; big-body scan test = 16
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16e"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16f"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -171,6 +171,24 @@ def pmc_traffic():
     return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(PMC_DEFAULT.relative_to(ROOT))
 
 
+def occupancy(ds, p, n_simd=1024, n_xcd=8):
+    """Resident waves per SIMD: the launch's limit (HIP occupancy query with its
+    dynamic LDS; VGPRs) and the measured mean over the timed kernel's launches
+    from the committed PMC pass (SQ_WAVE_CYCLES in 4-cycle units summed over
+    the SIMDs, vs GRBM_GUI_ACTIVE summed over the XCDs)."""
+    o = (C.c_int * 4)()
+    check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+    limit = min(8.0, o[0] * 4 / 4.0)   # 256-thread workgroups per CU x 4 waves / 4 SIMDs
+    res = {"limit_waves_per_simd": limit, "workgroups_per_cu": o[0], "vgprs": o[1], "lds_bytes_per_wg": o[2],
+           "lanes_per_pixel_shape": o[3], "hw_max_waves_per_simd": 8}
+    v = _pmc_avg(("waves",), ("SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"))
+    if v is not None:
+        mean = v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
+        res.update({"mean_waves_per_simd": mean, "frac_of_limit": mean / limit, "frac_of_hw_max": mean / 8.0,
+                    "source": str(PMC_DEFAULT.relative_to(ROOT))})
+    return res
+
+
 def pmc_valu(n_simd=1024, n_xcd=8):
     """VALU issue picture of the same launches: the fraction of cycles each
     SIMD issues a VALU instruction (SQ_ACTIVE_INST_VALU, 4-cycle units,
@@ -284,6 +302,7 @@ def main():
     segs_total, samples_total = tot.tolist()
     bvh = (bvh_counters(ds, cam, p, out, counters, sh, a.variant)
            if rank == 0 and lib.rt_resolve_variant(ds) in BVH_STATS else None)
+    occ = occupancy(ds, p) if rank == 0 else None
     lib.rt_scene_free(ds)
 
     if rank == 0:
@@ -330,10 +349,11 @@ def main():
                              "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
             "valu": pmc_valu(),
+            "occupancy": occ,
             "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
-            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 4x4-pixel sample pool per wave)" % a.variant,
+            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 8x8-pixel sample pool per workgroup)" % a.variant,
             "cpu_baseline": None,
         }
         if a.cpu_baseline == "auto" and world == 1:

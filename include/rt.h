@@ -206,6 +206,12 @@ int rt_set_variant(int variant);
  * fit): for reading the matching statistics build.  -1 on a NULL scene. */
 int rt_resolve_variant(const rt_dscene* ds);
 
+/* Occupancy of the launch rt_launch would make for (ds, p) under the current
+ * selectors (diagnostic): out4 = {256-thread workgroups per CU (HIP occupancy
+ * query with the launch's dynamic LDS), VGPRs per lane, LDS bytes per
+ * workgroup, lanes-per-pixel shape}. */
+int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int* out4);
+
 /* Launch shape.  1, 2, 4: lanes per pixel, each lane running a fixed share
  * of the pixel's four sample stripes.  -1 / -2: the sample pool, a wave owns
  * 4 x 4 / 8 x 8 pixels and every (pixel, sample) pair of them; a lane whose

@@ -1377,6 +1377,35 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
 
 extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_variant(*ds, g_variant) : -1; }
 
+// Occupancy of the launch rt_launch would make for (ds, p): the HIP occupancy
+// query on the kernel and dynamic LDS it would use (diagnostic, bench.py).
+extern "C" int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int* out4) {
+  clear_error();
+  if (!ds || !p || !out4) return set_error(RT_E_ARG, "rt_launch_occupancy: NULL argument");
+  const int rows = rows_out(*p);
+  if (rows <= 0 || p->width <= 0) return set_error(RT_E_ARG, "rt_launch_occupancy: empty frame");
+  HIP_TRY(hipSetDevice(ds->device));
+  const int vsel = resolve_variant(*ds, g_variant);
+  const DTree& tr = ds->tree[variant_tree(vsel)];
+  const Variant& v = variant_table(vsel);
+  const int lpp = choose_lpp(p->width, rows, p->spp, v);
+  const void* fn = v.fn[fn_slot(lpp)];
+  if (!fn) return set_error(RT_E_ARG, "rt_launch_occupancy: no launch shape");
+  const size_t lds = vsel >= 11 ? (v.lds ? lds_of(tr) : stack_of(tr))
+                                : (v.lds ? static_cast<size_t>(ds->n_pad) * sizeof(float4) : 0);
+  if (lds > 64 * 1024)
+    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  int blocks = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, lds));
+  hipFuncAttributes fa{};
+  HIP_TRY(hipFuncGetAttributes(&fa, fn));
+  out4[0] = blocks;               // 256-thread workgroups per CU
+  out4[1] = fa.numRegs;           // VGPRs per lane
+  out4[2] = static_cast<int>(lds + fa.sharedSizeBytes);   // LDS bytes per workgroup
+  out4[3] = lpp;
+  return RT_OK;
+}
+
 extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p, float* d_out,
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();

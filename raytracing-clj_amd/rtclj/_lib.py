@@ -79,6 +79,7 @@ SIGNATURES = {
                             C.c_void_p, C.c_void_p]),
     "rt_set_variant": (C.c_int, [C.c_int]),
     "rt_resolve_variant": (C.c_int, [C.c_void_p]),
+    "rt_launch_occupancy": (C.c_int, [C.c_void_p, C.POINTER(rt_params), C.POINTER(C.c_int)]),
     "rt_set_lanes_per_pixel": (C.c_int, [C.c_int]),
     "rt_set_schedule": (C.c_int, [C.c_int]),
     "rt_debug_stats": (C.c_int, [C.POINTER(C.c_uint64)]),

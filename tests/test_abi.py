@@ -121,6 +121,8 @@ def test_version_and_variant():
     assert rtclj.lib.rt_set_variant(old) == 2
     assert rtclj.lib.rt_set_variant(99) == old   # ignored
     assert rtclj.lib.rt_resolve_variant(None) == -1
+    out4 = (C.c_int * 4)()
+    assert rtclj.lib.rt_launch_occupancy(None, None, out4) < 0   # NULL scene: error, no device call
 
 
 def test_schedule_switch():
