@@ -46,8 +46,8 @@ from rtclj.shard import shard_params, shard_rows  # noqa: E402
 METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
 # executed fp32 flops (fma = 2) of the BVH traversal, per event:
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
-# exact body test (sqrt, root choice) = 4; big-body scan test = 16
-FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT, FLOPS_BODY = 24, 32, 4, 16
+# exact body test (sqrt, root choice) = 4
+FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT = 24, 32, 4
 PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16f"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
@@ -316,10 +316,11 @@ def main():
         bf_tflops = bf_flops / (kern_avg_ms * 1e-3) / 1e12
         if bvh is not None:
             per_seg = (FLOPS_NODE * bvh["nodes"] + FLOPS_LEAF_PAIR * bvh["leaf_pairs"] +
-                       FLOPS_EXACT * bvh["exact_tests"] + FLOPS_BODY * 1 + FLOPS_PER_SEGMENT)
+                       FLOPS_EXACT * bvh["exact_tests"] + FLOPS_PER_SEGMENT)
             work = (f"BVH traversal, executed fp32 work per segment = 24 x {bvh['nodes']:.2f} nodes + "
-                    f"32 x {bvh['leaf_pairs']:.2f} leaf pairs + 4 x {bvh['exact_tests']:.2f} exact tests + "
-                    f"16 (ground) + 100 = {per_seg:.0f} flops (counters: one untimed stats launch)")
+                    f"32 x {bvh['leaf_pairs']:.2f} leaf pairs (the big bodies' leaf included) + "
+                    f"4 x {bvh['exact_tests']:.2f} exact tests + 100 = {per_seg:.0f} flops "
+                    f"(counters: one untimed stats launch)")
         else:
             per_seg = FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT
             work = f"linear scan, executed fp32 work per segment = 17 x {len(scene)} bodies + 100"

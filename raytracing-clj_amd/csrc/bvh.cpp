@@ -9,8 +9,11 @@
 //     array order picks the lowest index among equal t);
 //   * the body test itself is the scan's fp32 op sequence;
 //   * boxes are culled only conservatively (per-ray padding, trace.hip).
-// "Big" bodies (radius > 16 x the median, e.g. the r = 1000 ground) would
-// make every box huge; they are kept out of the tree and scanned first.
+// "Big" bodies (up to kBvhBigMax bodies of radius > 4 x the median, e.g. the
+// r = 1000 ground and the cover scene's three r = 1 spheres) would make the
+// boxes around them loose; they are kept out of the tree and tested as extra
+// leaves before every traversal (a 4-body leaf costs the wave about what one
+// scalar body test did, tools/simt_sim.cpp priced the tighter tree at -15 %).
 //
 // Layout (device, all 16-byte aligned):
 //   nodes[n_nodes]   BvhNode: child boxes as (c0, c1) float pairs for packed
@@ -23,6 +26,8 @@
 //                    a missing body has w = +inf: never a candidate); a leaf
 //                    is 1 pair (leaf_size 2) or 2 consecutive pairs (4)
 //   pidx[n_pairs]    original indices of the two bodies (-1 for the pad)
+//   the big bodies' leaves follow the tree's in pairs / pidx (big_pair0,
+//   n_big_leaves)
 #include "bvh.h"
 
 #include <algorithm>
@@ -31,6 +36,8 @@
 #include <numeric>
 
 namespace rtclj {
+
+float g_bvh_big_ratio = 4.0f;    // big-body threshold (x the median radius); tools/simt_sim.cpp
 
 namespace {
 
@@ -204,14 +211,34 @@ int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size, bool sah) {
   Builder b{sph, {}, out};
   b.leaf_size = leaf_size;
   b.sah = sah;
+  // non-finite bodies (no box) and the kBvhBigMax largest bodies of radius >
+  // g_bvh_big_ratio x the median (the r = 1000 ground, the cover scene's three
+  // r = 1 spheres: their boxes would enclose many small bodies' boxes)
+  std::vector<char> is_big(n, 0);
   for (int i = 0; i < n; ++i) {
     const bool finite = std::isfinite(sph[4 * i]) && std::isfinite(sph[4 * i + 1]) &&
                         std::isfinite(sph[4 * i + 2]) && std::isfinite(sph[4 * i + 3]);
-    if (!finite || (n > 8 && radii[i] > 16.0f * med && out->big.size() < 64))
+    if (!finite && out->big.size() < 64) {
+      is_big[i] = 1;
       out->big.push_back(i);
-    else
-      b.prim.push_back(i);
+    }
   }
+  if (n > 8) {
+    std::vector<int> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return radii[x] > radii[y]; });
+    int added = 0;
+    for (int i : order) {
+      if (added == kBvhBigMax || !(radii[i] > g_bvh_big_ratio * med)) break;
+      if (is_big[i]) continue;
+      is_big[i] = 1;
+      out->big.push_back(i);
+      ++added;
+    }
+  }
+  std::sort(out->big.begin(), out->big.end());
+  for (int i = 0; i < n; ++i)
+    if (!is_big[i]) b.prim.push_back(i);
   // bounding sphere of the tree's bodies (centre of their box, radius to the
   // farthest surface): D = |O - centre| + radius bounds |oc| + r per ray
   Box all;
@@ -263,6 +290,16 @@ int bvh_build(const float* sph, int n, BvhHost* out, int leaf_size, bool sah) {
       }
   }
   out->depth = b.max_depth + 1;
+  // the big bodies as leaves after the tree's (same pair layout, padded with
+  // never-hit bodies): the kernel tests them with the leaf test, every segment
+  out->big_pair0 = static_cast<int>(out->pidx.size() / 2);
+  const int nb = static_cast<int>(out->big.size());
+  b.prim.insert(b.prim.end(), out->big.begin(), out->big.end());
+  for (int q = 0; q < nb; q += leaf_size) {
+    Box unused;
+    b.leaf(cnt + q, std::min(leaf_size, nb - q), &unused);
+    ++out->n_big_leaves;
+  }
   return 0;
 }
 

@@ -19,7 +19,9 @@ struct BvhHost {
   std::vector<BvhNode> nodes;
   std::vector<float> pairs;   // 8 floats per leaf pair
   std::vector<int> pidx;      // 2 original indices per leaf pair (-1: pad)
-  std::vector<int> big;       // bodies scanned before the traversal, ascending
+  std::vector<int> big;       // bodies tested before the traversal, ascending
+  int big_pair0 = 0;          // their leaves: pairs [big_pair0, + n_big_leaves x leaf pairs)
+  int n_big_leaves = 0;
   float center[3] = {0, 0, 0};
   float radius = 0.0f;        // bounding sphere of the tree's bodies
   int depth = 0;              // levels of nodes on the longest root-leaf path
@@ -30,6 +32,8 @@ struct BvhHost {
 // depth + 2 <= kBvhStack (surface-area splits where the depth allows, median
 // splits below: depth <= ceil(log2(n/2)) + 1 = 13 for 8192 bodies)
 constexpr int kBvhStack = 16;
+// bodies kept out of the tree for their size (besides non-finite ones)
+constexpr int kBvhBigMax = 8;
 
 // sah: surface-area-heuristic splits (else median splits)
 int bvh_build(const float* sphere, int n, BvhHost* out, int leaf_size = 2, bool sah = true);

@@ -67,11 +67,11 @@ struct alignas(16) KArgs {
   int row_begin, row_tile, tile_first, tile_step;
   // BVH traversal (SCAN_BVH): blob = nodes | pairs | pidx (the LDS image)
   const float4* bvh_blob;
-  const int* bvh_big;    // bodies scanned before the traversal (ascending)
   int bvh_blob_f4;       // blob size in float4
   int bvh_off_pairs;     // byte offsets inside the blob
   int bvh_off_pidx;
-  int n_big;
+  int big_pair0;         // the big bodies' leaves (bvh.cpp): pairs [big_pair0, + n_big_leaves x leaf pairs)
+  int n_big_leaves;
   int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
@@ -418,17 +418,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         best_t = acc ? t : best_t;
         best = acc ? s : best;
       };
-      // 1) big bodies (kept out of the tree), ascending index
-      for (int i = 0; i < a.n_big; ++i) {
-        const int s = a.bvh_big[i];
-        const float4 g = a.geo[s];
-        const float ocx = g.x - ox, ocy = g.y - oy, ocz = g.z - oz;
-        const float h = fmaf(uz, ocz, fmaf(uy, ocy, ux * ocx));
-        const float c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
-        const float disc = fmaf(h, h, -c);
-        if (fminf(disc, fmaxf(h, -c)) >= 0.0f) consider_tie(h, disc, s);
-      }
-      // 2) the tree
+      // 1) the big bodies, kept out of the tree (bvh.cpp), as leaves of their
+      // own (below), 2) the tree
       const char* base = SRC == SRC_LDS ? reinterpret_cast<const char*>(s_geo)
                                         : reinterpret_cast<const char*>(a.bvh_blob);
       const KNode* nodes = reinterpret_cast<const KNode*>(base);
@@ -535,6 +526,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         c0 = ch.x;
         c1 = ch.y;
       };
+      // the big bodies' leaves first: every lane, so a wave-uniform loop (their
+      // hits, e.g. the ground, then cull the tree)
+      for (int b = 0; b < a.n_big_leaves; ++b) leaf(a.big_pair0 + b * leaf_pairs(SCAN));
       if constexpr (SCAN == SCAN_BVHWW) {
         // speculative while-while (Aila & Laine 2009): a node phase in which
         // a lane that already holds a leaf keeps descending until every lane
@@ -1159,11 +1153,10 @@ static unsigned long long* g_dbgw = nullptr;  // device u64[4 * 65536] wave time
 
 using namespace rtclj;
 
-// one BVH on the device: blob = nodes | pairs | pidx, and the big-body list
+// one BVH on the device: blob = nodes | pairs | pidx (the big bodies' leaves after the tree's)
 struct DTree {
   float4* blob;
-  int* big;
-  int blob_f4, off_pairs, off_pidx, n_big, depth;
+  int blob_f4, off_pairs, off_pidx, big_pair0, n_big_leaves, depth;
   float c[3], r;
 };
 
@@ -1308,20 +1301,17 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     std::memcpy(blob.data(), bvh.nodes.data(), nb);
     std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
     std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
-    std::vector<int> big = bvh.big;
-    if (big.empty()) big.push_back(0);
     DTree& t = d->tree[k];
     t.blob_f4 = static_cast<int>(blob.size() / 16);
     t.off_pairs = static_cast<int>(nb);
     t.off_pidx = static_cast<int>(nb + pb);
-    t.n_big = static_cast<int>(bvh.big.size());
+    t.big_pair0 = bvh.big_pair0;
+    t.n_big_leaves = bvh.n_big_leaves;
     t.depth = bvh.depth;
     for (int j = 0; j < 3; ++j) t.c[j] = bvh.center[j];
     t.r = bvh.radius;
     e = hipMalloc(&t.blob, blob.size());
     if (e == hipSuccess) e = hipMemcpy(t.blob, blob.data(), blob.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&t.big, big.size() * sizeof(int));
-    if (e == hipSuccess) e = hipMemcpy(t.big, big.data(), big.size() * sizeof(int), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMalloc(&d->geo2, n_pad * sizeof(float4));
   if (e == hipSuccess) e = hipMemcpy(d->geo2, geo2.data(), n_pad * sizeof(float4), hipMemcpyHostToDevice);
@@ -1347,7 +1337,6 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   if (d->geo2) (void)hipFree(d->geo2);
   for (const DTree& t : d->tree) {
     if (t.blob) (void)hipFree(t.blob);
-    if (t.big) (void)hipFree(t.big);
   }
   d->sched.release();
   if (d->sph) (void)hipFree(d->sph);
@@ -1451,11 +1440,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   const Variant& v = variant_table(vsel);
   const bool is_bvh = vsel >= 11;
   a.bvh_blob = tr.blob;
-  a.bvh_big = tr.big;
   a.bvh_blob_f4 = tr.blob_f4;
   a.bvh_off_pairs = tr.off_pairs;
   a.bvh_off_pidx = tr.off_pidx;
-  a.n_big = tr.n_big;
+  a.big_pair0 = tr.big_pair0;
+  a.n_big_leaves = tr.n_big_leaves;
   a.bvh_stack = tr.depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""A/B whole library builds on one GPU: alternates `bench.py` runs (one
+process each, RTCLJ_LIBRARY selects the build) for R rounds and prints the
+median kernel ms per build.  Every run has its own time limit; the first
+failing run ends the script (no retries).
+
+  python tools/ab_libs.py --libs raytracing-clj_amd/lib/ab_base.so raytracing-clj_amd/lib/librtclj.so \
+      --rounds 3 [--out gpurun_out/ab.jsonl] [-- extra bench.py args]
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def main():
+    argv = sys.argv[1:]
+    extra = []
+    if "--" in argv:
+        k = argv.index("--")
+        argv, extra = argv[:k], argv[k + 1:]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    res = {lib: [] for lib in a.libs}
+    out = open(a.out, "a") if a.out else None
+    for r in range(a.rounds):
+        for lib in a.libs:
+            env = dict(os.environ, RTCLJ_LIBRARY=str(Path(lib).resolve()))
+            cmd = [sys.executable, str(ROOT / "bench.py"), "--cpu-baseline", "off", "--steps", str(a.steps),
+                   "--warmup", "2"] + extra
+            p = subprocess.run(["timeout", "-k", "10", "240"] + cmd, env=env, capture_output=True, text=True)
+            if p.returncode != 0:
+                print(f"run failed ({p.returncode}) for {lib}:\n{p.stderr[-3000:]}", flush=True)
+                sys.exit(p.returncode)
+            line = json.loads(p.stdout.strip().splitlines()[-1])
+            ms = line["kernel_ms_avg"]
+            res[lib].append(ms)
+            print(f"round {r} {Path(lib).name:24s} kernel {ms:.3f} ms  {line['value']:.0f} Msamples/s", flush=True)
+            if out:
+                out.write(json.dumps({"round": r, "lib": Path(lib).name, "kernel_ms_avg": ms,
+                                      "value": line["value"], "bvh": line.get("bvh_per_segment"),
+                                      "args": extra}) + "\n")
+                out.flush()
+    for lib, v in res.items():
+        print(f"{Path(lib).name:24s} median {statistics.median(v):.3f} ms  min {min(v):.3f}  runs {v}")
+
+
+if __name__ == "__main__":
+    main()

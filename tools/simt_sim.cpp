@@ -1,0 +1,389 @@
+// simt_sim.cpp — design tool (not product code): a CPU model of the trace
+// kernel's SIMT cost on the C1 workload, to compare ways of grouping paths
+// into waves before building one on the GPU.
+//
+// It traces the cover scene with the kernel's semantics in fp32 (not bit
+// exact: no padding, plain sqrt; the work counts are what matters) through
+// the same 4-body-leaf SAH tree (bvh.cpp), and records per segment the
+// traversal as the kernel runs it: node visits, and per visit the leaves
+// entered and their candidate bodies.  A wave's cost for one outer iteration
+// is then priced the way the hardware issues it (VALU issue
+// bound, a wave pays for a block if any lane needs it):
+//   outer       C_OUT per wave iteration (camera, setup, shading)
+//   traversal   sum over steps i < max lanes' visits of
+//               C_NODE + C_LEAF * max_lanes(leaves at i) + C_EXACT * max_lanes(cands)
+// Policies:
+//   wave   the shipped shape: a workgroup's 8x8-pixel pool, 4 independent
+//          waves refilling from it (advanced in cost order)
+//   sort   the 4 waves advance together; before every iteration the 256
+//          paths are sorted by a key and dealt to the waves in that order
+//
+//   g++ -O2 -std=c++17 -I include tools/simt_sim.cpp raytracing-clj_amd/csrc/bvh.cpp \
+//       -Lraytracing-clj_amd/lib -lrtclj -Wl,-rpath,$PWD/raytracing-clj_amd/lib -o /tmp/simt_sim
+//   /tmp/simt_sim [tiles=300] [spp=100]
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <numeric>
+#include <vector>
+
+#include "../include/rt.h"
+#include "../raytracing-clj_amd/csrc/bvh.h"
+
+using namespace rtclj;
+namespace rtclj { extern float g_bvh_big_ratio; }
+static double g_cand = 0, g_rej = 0;
+
+static const double C_OUT = 400, C_NODE = 38, C_LEAF = 45, C_EXACT = 44, C_SORT = 60;
+
+static uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+struct Rng {
+  uint32_t s;
+  float u() { s ^= s << 13; s ^= s >> 17; s ^= s << 5; return float(s >> 8) * 0x1p-24f; }
+  float sym() { return 2.0f * u() - 1.0f; }
+};
+
+struct Scene {
+  int n;
+  std::vector<float> sph, mat;
+  std::vector<int> kind;
+  BvhHost t;
+};
+
+// one segment's traversal as the kernel runs it
+struct Trav {
+  std::vector<uint8_t> leaves;   // per visit: leaves entered (0-2)
+  std::vector<uint8_t> c1, c2;   // per visit: candidates in the first / second leaf
+};
+
+struct Hit { int body; float t; };
+
+static void body_test(const float* s, float ox, float oy, float oz, float ux, float uy, float uz,
+                      float tmin, int last, Hit& best, int idx, int& cand) {
+  const float ocx = s[0] - ox, ocy = s[1] - oy, ocz = s[2] - oz;
+  const float h = ux * ocx + uy * ocy + uz * ocz;
+  const float c = ocx * ocx + ocy * ocy + ocz * ocz - s[3] * s[3];
+  const float disc = h * h - c;
+  if (!(std::fmin(disc, std::fmax(h, -c)) >= 0.0f)) return;
+  ++cand;
+  g_cand += 1;
+  const float sq = idx == last ? std::fabs(h) : std::sqrt(disc);
+  float t = h - sq;
+  if (!(t > tmin)) t = h + sq;
+  if (t > tmin && (t < best.t || (t == best.t && idx < best.body))) best = {idx, t};
+  else if (h - std::sqrt(disc) >= best.t) g_rej += 1;   // a near root beyond the best: a t-bound filter drops it
+}
+
+static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float uy, float uz, float tmin, int last,
+                 Trav* tr) {
+  Hit best{-1, INFINITY};
+  int dummy = 0;
+  for (int b : S.t.big) body_test(&S.sph[4 * b], ox, oy, oz, ux, uy, uz, tmin, last, best, b, dummy);
+  const float ex = ox - S.t.center[0], ey = oy - S.t.center[1], ez = oz - S.t.center[2];
+  const float rx = 1.0f / (std::fabs(ux) < 1e-24f ? std::copysign(1e-24f, ux) : ux);
+  const float ry = 1.0f / (std::fabs(uy) < 1e-24f ? std::copysign(1e-24f, uy) : uy);
+  const float rz = 1.0f / (std::fabs(uz) < 1e-24f ? std::copysign(1e-24f, uz) : uz);
+  auto leaf = [&](int p, int& cand) {
+    for (int q = 0; q < 2; ++q)
+      for (int j = 0; j < 2; ++j) {
+        const int id = S.t.pidx[2 * (p + q) + j];
+        if (id < 0) continue;
+        body_test(&S.sph[4 * id], ox, oy, oz, ux, uy, uz, tmin, last, best, id, cand);
+      }
+  };
+  int stack[64], sp = 0, node = 0;
+  for (;;) {
+    const BvhNode& nd = S.t.nodes[node];
+    float tn[2], tf[2];
+    bool hit[2];
+    for (int c = 0; c < 2; ++c) {
+      const float x0 = (nd.x[c] - ex) * rx, x1 = (nd.x[2 + c] - ex) * rx;
+      const float y0 = (nd.y[c] - ey) * ry, y1 = (nd.y[2 + c] - ey) * ry;
+      const float z0 = (nd.z[c] - ez) * rz, z1 = (nd.z[2 + c] - ez) * rz;
+      tn[c] = std::max({std::min(x0, x1), std::min(y0, y1), std::min(z0, z1)});
+      tf[c] = std::min({std::max(x0, x1), std::max(y0, y1), std::max(z0, z1)});
+      hit[c] = std::max(tn[c], tmin) <= std::min(tf[c], best.t);
+    }
+    const int c0 = nd.child[0], c1 = nd.child[1];
+    const bool l0 = hit[0] && c0 < 0, l1 = hit[1] && c1 < 0;
+    int k1 = 0, k2 = 0;
+    if (l0 | l1) leaf(l0 ? ~c0 : ~c1, k1);
+    if (l0 & l1) leaf(~c1, k2);
+    if (tr) {
+      tr->leaves.push_back(uint8_t(l0 + l1));
+      tr->c1.push_back(uint8_t(k1));
+      tr->c2.push_back(uint8_t(k2));
+    }
+    const bool h0 = hit[0] && !l0, h1 = hit[1] && !l1;
+    if (h0 && h1) {
+      const bool sw = tn[1] < tn[0];
+      stack[sp++] = sw ? c0 : c1;
+      node = sw ? c1 : c0;
+    } else if (h0) {
+      node = c0;
+    } else if (h1) {
+      node = c1;
+    } else {
+      if (sp == 0) break;
+      node = stack[--sp];
+    }
+  }
+  return best;
+}
+
+// a path in flight: the lane state of the kernel's outer loop
+struct Path {
+  int j = -1;          // pool index (-1: lane idle)
+  Rng rng{1};
+  float o[3], d[3];
+  int rem = 0, last = -1;
+  bool fresh = true;
+};
+
+struct Ctx {
+  const Scene* S;
+  rt_camera cam;
+  int width, spp, depth;
+};
+
+// one outer iteration of a lane: camera (if fresh), the segment, shading.
+// Returns true when the path ended (the lane takes a new pool index).
+static bool step(const Ctx& C, Path& p, int px, int py, Trav& tr) {
+  const Scene& S = *C.S;
+  if (p.fresh) {
+    const uint32_t key = mix32(1u);
+    const uint32_t pk = mix32(key ^ mix32(uint32_t(py) * uint32_t(C.width) + uint32_t(px)));
+    const int k = p.j % C.spp;
+    p.rng.s = mix32(pk + uint32_t(k) * 0x9e3779b9u);
+    if (!p.rng.s) p.rng.s = 0x6d2b79f5u;
+    const float fx = float(px) + (p.rng.u() - 0.5f), fy = float(py) + (p.rng.u() - 0.5f);
+    float s[3], o[3];
+    for (int a = 0; a < 3; ++a) s[a] = C.cam.p00[a] + C.cam.du[a] * fx + C.cam.dv[a] * fy;
+    float qx, qy;
+    do { qx = p.rng.sym(); qy = p.rng.sym(); } while (!(qx * qx + qy * qy < 1.0f));
+    for (int a = 0; a < 3; ++a) o[a] = C.cam.center[a] + C.cam.disk_u[a] * qx + C.cam.disk_v[a] * qy;
+    for (int a = 0; a < 3; ++a) { p.o[a] = o[a]; p.d[a] = s[a] - o[a]; }
+    p.rem = C.depth;
+    p.last = -1;
+    p.fresh = false;
+  }
+  --p.rem;
+  const float len = std::sqrt(p.d[0] * p.d[0] + p.d[1] * p.d[1] + p.d[2] * p.d[2]);
+  const float u[3] = {p.d[0] / len, p.d[1] / len, p.d[2] / len};
+  const Hit h = trace(S, p.o[0], p.o[1], p.o[2], u[0], u[1], u[2], 1e-3f * len, p.last, &tr);
+  if (h.body < 0 || p.rem == 0) return true;
+  const float* c = &S.sph[4 * h.body];
+  float hp[3], n[3];
+  for (int a = 0; a < 3; ++a) hp[a] = p.o[a] + u[a] * h.t;
+  for (int a = 0; a < 3; ++a) n[a] = (hp[a] - c[a]) / c[3];
+  const bool front = p.d[0] * n[0] + p.d[1] * n[1] + p.d[2] * n[2] < 0.0f;
+  if (!front) for (float& x : n) x = -x;
+  for (int a = 0; a < 3; ++a) p.o[a] = hp[a];
+  p.last = h.body;
+  const int kind = S.kind[h.body];
+  const float* m = &S.mat[4 * h.body];
+  if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
+    float q[3], l2;
+    do { q[0] = p.rng.sym(); q[1] = p.rng.sym(); q[2] = p.rng.sym(); l2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2]; }
+    while (!(l2 > 0.0f && l2 <= 1.0f));
+    const float il = 1.0f / std::sqrt(l2);
+    for (float& x : q) x *= il;
+    if (kind == RT_LAMBERTIAN) {
+      for (int a = 0; a < 3; ++a) p.d[a] = q[a] + n[a];
+    } else {
+      const float k2 = 2.0f * (p.d[0] * n[0] + p.d[1] * n[1] + p.d[2] * n[2]);
+      float r[3];
+      for (int a = 0; a < 3; ++a) r[a] = p.d[a] - n[a] * k2 + m[3] * q[a];
+      if (!(r[0] * n[0] + r[1] * n[1] + r[2] * n[2] > 0.0f)) return true;
+      for (int a = 0; a < 3; ++a) p.d[a] = r[a];
+    }
+  } else {
+    const float ri = front ? 1.0f / m[3] : m[3];
+    const float un = u[0] * n[0] + u[1] * n[1] + u[2] * n[2];
+    const float cosv = std::fmin(-un, 1.0f), sinv = std::sqrt(1.0f - cosv * cosv);
+    bool refl = !(ri * sinv <= 1.0f);
+    if (!refl) {
+      const float xi = p.rng.u();
+      float r0 = (1.0f - ri) / (1.0f + ri);
+      r0 *= r0;
+      const float x1 = 1.0f - cosv;
+      refl = r0 + (1.0f - r0) * x1 * x1 * x1 * x1 * x1 > xi;
+    }
+    if (refl) {
+      for (int a = 0; a < 3; ++a) p.d[a] = u[a] - n[a] * 2.0f * un;
+    } else {
+      float q[3];
+      for (int a = 0; a < 3; ++a) q[a] = (u[a] + n[a] * cosv) * ri;
+      const float par = -std::sqrt(std::fabs(1.0f - (q[0] * q[0] + q[1] * q[1] + q[2] * q[2])));
+      for (int a = 0; a < 3; ++a) p.d[a] = q[a] + n[a] * par;
+    }
+  }
+  return false;
+}
+
+// wave cost of one outer iteration over the lanes' segments
+static double g_leaf_passes = 0, g_exact_passes = 0;
+static double wave_cost(const std::vector<const Trav*>& lanes, double* node_steps) {
+  if (lanes.empty()) return 0.0;
+  size_t L = 0;
+  for (const Trav* t : lanes) L = std::max(L, t->leaves.size());
+  double c = C_OUT;
+  for (size_t i = 0; i < L; ++i) {
+    int ml = 0, m1 = 0, m2 = 0;
+    for (const Trav* t : lanes)
+      if (i < t->leaves.size()) {
+        ml = std::max<int>(ml, t->leaves[i]);
+        m1 = std::max<int>(m1, t->c1[i]);
+        m2 = std::max<int>(m2, t->c2[i]);
+      }
+    c += C_NODE + C_LEAF * ml + C_EXACT * (m1 + m2);
+    g_leaf_passes += ml;
+    g_exact_passes += m1 + m2;
+  }
+  *node_steps += double(L);
+  return c;
+}
+
+struct Result { double cost = 0, iters = 0, steps = 0, samples = 0, lane_steps = 0; };
+
+// one workgroup tile (8x8 pixels at (tx, ty)) under a policy
+static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Result& R) {
+  const int npx = 64, pool = npx * C.spp;
+  std::vector<Path> lanes(256);
+  int next = 0;
+  for (int l = 0; l < 256; ++l) lanes[l].j = next < pool ? next++ : -1;
+  auto pixel = [&](int j, int& px, int& py) {
+    const int q = j / C.spp;
+    px = tx * 8 + q % 8;
+    py = ty * 8 + q / 8;
+  };
+  R.samples += pool;
+  if (policy == 0) {
+    // 4 independent waves, advanced in order of accumulated cost
+    double wc[4] = {0, 0, 0, 0};
+    for (;;) {
+      int w = -1;
+      for (int k = 0; k < 4; ++k) {
+        bool any = false;
+        for (int l = 0; l < 64; ++l) any |= lanes[64 * k + l].j >= 0;
+        if (any && (w < 0 || wc[k] < wc[w])) w = k;
+      }
+      if (w < 0) break;
+      std::vector<Trav> tr(64);
+      std::vector<const Trav*> act;
+      std::vector<int> done;
+      for (int l = 0; l < 64; ++l) {
+        Path& p = lanes[64 * w + l];
+        if (p.j < 0) continue;
+        int px, py;
+        pixel(p.j, px, py);
+        if (step(C, p, px, py, tr[l])) done.push_back(l);
+        act.push_back(&tr[l]);
+        R.lane_steps += tr[l].leaves.size();
+      }
+      const double c = wave_cost(act, &R.steps);
+      wc[w] += c;
+      R.cost += c;
+      R.iters += 1;
+      for (int l : done) {
+        Path& p = lanes[64 * w + l];
+        p = Path{};
+        p.j = next < pool ? next++ : -1;
+      }
+    }
+  } else {
+    // all 256 lanes step together; paths dealt to waves sorted by key
+    for (;;) {
+      std::vector<int> live;
+      for (int l = 0; l < 256; ++l)
+        if (lanes[l].j >= 0) live.push_back(l);
+      if (live.empty()) break;
+      std::vector<int> oracle_len(256, 0);
+      if (key_mode == 3)   // upper bound: the segment's own visit count (traced on a copy)
+        for (int l : live) {
+          Path cp = lanes[l];
+          Trav t;
+          int px, py;
+          pixel(cp.j, px, py);
+          step(C, cp, px, py, t);
+          oracle_len[l] = int(t.leaves.size());
+        }
+      auto key = [&](const Path& p) -> int {
+        if (key_mode == 3) return oracle_len[&p - lanes.data()];
+        if (p.fresh) return 0;   // camera rays first (coherent already)
+        const int oct = (p.d[0] < 0) | ((p.d[1] < 0) << 1) | ((p.d[2] < 0) << 2);
+        if (key_mode == 1) return 1 + oct;
+        if (key_mode == 2) return 1 + oct * 64 + ((p.last & 63));  // octant, then the body left
+        return 1 + oct;
+      };
+      std::stable_sort(live.begin(), live.end(), [&](int a, int b) { return key(lanes[a]) < key(lanes[b]); });
+      std::vector<Trav> tr(256);
+      std::vector<int> done;
+      for (size_t w = 0; w * 64 < live.size(); ++w) {
+        std::vector<const Trav*> act;
+        for (size_t i = w * 64; i < std::min(live.size(), w * 64 + 64); ++i) {
+          const int l = live[i];
+          Path& p = lanes[l];
+          int px, py;
+          pixel(p.j, px, py);
+          if (step(C, p, px, py, tr[l])) done.push_back(l);
+          act.push_back(&tr[l]);
+          R.lane_steps += tr[l].leaves.size();
+        }
+        R.cost += wave_cost(act, &R.steps) + C_SORT;
+        R.iters += 1;
+      }
+      for (int l : done) {
+        lanes[l] = Path{};
+        lanes[l].j = next < pool ? next++ : -1;
+      }
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const int tiles = argc > 1 ? std::atoi(argv[1]) : 300;
+  const int spp = argc > 2 ? std::atoi(argv[2]) : 100;
+  Scene S;
+  S.n = rt_scene_cover(11, 42, nullptr, nullptr, nullptr, 0);
+  S.sph.resize(4 * S.n);
+  S.mat.resize(4 * S.n);
+  S.kind.resize(S.n);
+  rt_scene_cover(11, 42, S.sph.data(), S.kind.data(), S.mat.data(), S.n);
+  if (std::getenv("BIG")) g_bvh_big_ratio = std::atof(std::getenv("BIG"));
+  bvh_build(S.sph.data(), S.n, &S.t, 4, true);
+  std::printf("tree: %zu nodes, depth %d, big %zu\n", S.t.nodes.size(), S.t.depth, S.t.big.size());
+  Ctx C{&S, {}, 1200, spp, 50};
+  const double lf[3] = {13, 2, 3}, la[3] = {0, 0, 0}, vup[3] = {0, 1, 0};
+  rt_camera_setup(1200, 675, 20.0, lf, la, vup, 0.6, 10.0, &C.cam);
+  const int gx = 1200 / 8, gy = (675 + 7) / 8;
+  std::vector<int> pick;
+  uint32_t h = 12345;
+  for (int i = 0; i < tiles; ++i) {
+    h = mix32(h + 1);
+    pick.push_back(int(h % uint32_t(gx * (gy - 1))));
+  }
+  const char* names[] = {"wave (shipped)", "sort by octant", "sort by octant+body", "sort by visits (bound)"};
+  const int pol[] = {0, 1, 1, 1}, km[] = {0, 1, 2, 3};
+  const int nv = std::getenv("NV") ? std::atoi(std::getenv("NV")) : 4;
+  for (int v = 0; v < nv; ++v) {
+    Result R;
+    g_leaf_passes = g_exact_passes = 0;
+    for (int t : pick) run_tile(C, t % gx, t / gx, pol[v], km[v], R);
+    std::printf("  per wave-iter: node steps %.2f leaf passes %.2f exact passes %.2f  (cost shares: outer %.2f node %.2f leaf %.2f exact %.2f)\n",
+                R.steps / R.iters, g_leaf_passes / R.iters, g_exact_passes / R.iters,
+                C_OUT * R.iters / R.cost, C_NODE * R.steps / R.cost, C_LEAF * g_leaf_passes / R.cost,
+                C_EXACT * g_exact_passes / R.cost);
+    std::printf("  candidates rejected by the t bound: %.3f of %.0f\n", g_rej / g_cand, g_cand);
+    g_rej = g_cand = 0;
+    std::printf("%-22s cost/sample %8.1f  wave-iters/sample %.3f  trav steps/wave-iter %.2f  lane eff %.3f\n",
+                names[v], R.cost / R.samples, R.iters / R.samples * 64, R.steps / R.iters,
+                R.lane_steps / (R.steps * 64));
+  }
+  return 0;
+}
