@@ -610,26 +610,25 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         node_test(node, tn0, tn1, hit0, hit1, c0, c1);
         // leaf children are tested now; a lane's first leaf shares one pass
         // with every other lane's first leaf, whichever child it is
-        const bool l0 = hit0 & (c0 < 0), l1 = hit1 & (c1 < 0);
-        if (l0 | l1) {
+        const bool l0 = hit0 && c0 < 0, l1 = hit1 && c1 < 0;
+        if (l0 || l1) {
           leaf(l0 ? ~c0 : ~c1);
-          if (l0 & l1) leaf(~c1);
+          if (l0 && l1) leaf(~c1);
         }
-        hit0 = hit0 & !l0;
-        hit1 = hit1 & !l1;
-        if (hit0 && hit1) {
-          const bool sw = tn1 < tn0;
-          s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? c0 : c1);
-          ++sp;
-          node = sw ? c1 : c0;
-        } else if (hit0) {
-          node = c0;
-        } else if (hit1) {
-          node = c1;
-        } else {
+        // inner children: both -> the near one next, the far one pushed; one
+        // -> that one; none -> pop.  The far child is written above the stack
+        // top every step (a dead entry unless both were hit): no branch
+        const bool i0 = hit0 && c0 >= 0, i1 = hit1 && c1 >= 0;
+        const bool sw = tn1 < tn0;
+        const int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
+        s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? c0 : c1);
+        sp += (i0 && i1) ? 1 : 0;
+        if (!(i0 || i1)) {
           if (sp == 0) break;
           --sp;
           node = s_stack[sp * 256 + threadIdx.x];
+        } else {
+          node = nxt;
         }
       }
       }

@@ -34,9 +34,19 @@
 
 using namespace rtclj;
 namespace rtclj { extern float g_bvh_big_ratio; }
-static double g_cand = 0, g_rej = 0;
+static double g_cand = 0, g_rej = 0, g_segs = 0, g_visits = 0, g_leafs = 0;
+static float g_pad = 1.0f;
+static int g_big_leaves = 0;
+static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
+static double C_EXACT_B = 32;
 
-static const double C_OUT = 400, C_NODE = 38, C_LEAF = 45, C_EXACT = 44, C_SORT = 60;
+// VALU wave-instructions per block (from the ISA of the default kernel,
+// trace_kernel<1, 5, -3, false>); leaf and exact costs for NP body pairs per leaf
+static double C_OUT = 356, C_NODE = 38, C_LEAF = 45, C_EXACT = 44, C_SORT = 60;
+static void set_leaf_costs(int np) {
+  C_LEAF = 20 + 12.5 * np;
+  C_EXACT = 35 + 3 * (2 * np - 1);
+}
 
 static uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
@@ -57,12 +67,14 @@ struct Scene {
 
 // one segment's traversal as the kernel runs it
 struct Trav {
+  int big_c = 0;                 // candidate bitmask of the big bodies (their leaf pass: every segment)
   std::vector<uint8_t> leaves;   // per visit: leaves entered (0-2)
-  std::vector<uint8_t> c1, c2;   // per visit: candidates in the first / second leaf
+  std::vector<uint8_t> c1, c2;   // per visit: candidate bitmasks of the first / second leaf
 };
 
 struct Hit { int body; float t; };
 
+static int g_candbit = 0;   // the body's position in its leaf (candidate bitmask)
 static void body_test(const float* s, float ox, float oy, float oz, float ux, float uy, float uz,
                       float tmin, int last, Hit& best, int idx, int& cand) {
   const float ocx = s[0] - ox, ocy = s[1] - oy, ocz = s[2] - oz;
@@ -70,7 +82,7 @@ static void body_test(const float* s, float ox, float oy, float oz, float ux, fl
   const float c = ocx * ocx + ocy * ocy + ocz * ocz - s[3] * s[3];
   const float disc = h * h - c;
   if (!(std::fmin(disc, std::fmax(h, -c)) >= 0.0f)) return;
-  ++cand;
+  cand |= 1 << g_candbit;
   g_cand += 1;
   const float sq = idx == last ? std::fabs(h) : std::sqrt(disc);
   float t = h - sq;
@@ -82,29 +94,39 @@ static void body_test(const float* s, float ox, float oy, float oz, float ux, fl
 static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float uy, float uz, float tmin, int last,
                  Trav* tr) {
   Hit best{-1, INFINITY};
-  int dummy = 0;
-  for (int b : S.t.big) body_test(&S.sph[4 * b], ox, oy, oz, ux, uy, uz, tmin, last, best, b, dummy);
+  int bigc = 0;
+  for (size_t i = 0; i < S.t.big.size(); ++i) {
+    g_candbit = int(i);
+    body_test(&S.sph[4 * S.t.big[i]], ox, oy, oz, ux, uy, uz, tmin, last, best, S.t.big[i], bigc);
+  }
+  if (tr) tr->big_c = bigc;
   const float ex = ox - S.t.center[0], ey = oy - S.t.center[1], ez = oz - S.t.center[2];
+  const float D = std::sqrt(ex * ex + ey * ey + ez * ez) + S.t.radius;
+  const float P = g_pad * 2e-3f * D;
   const float rx = 1.0f / (std::fabs(ux) < 1e-24f ? std::copysign(1e-24f, ux) : ux);
   const float ry = 1.0f / (std::fabs(uy) < 1e-24f ? std::copysign(1e-24f, uy) : uy);
   const float rz = 1.0f / (std::fabs(uz) < 1e-24f ? std::copysign(1e-24f, uz) : uz);
+  const int np = S.t.leaf_size / 2;
   auto leaf = [&](int p, int& cand) {
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < np; ++q)
       for (int j = 0; j < 2; ++j) {
         const int id = S.t.pidx[2 * (p + q) + j];
         if (id < 0) continue;
+        g_candbit = 2 * q + j;
         body_test(&S.sph[4 * id], ox, oy, oz, ux, uy, uz, tmin, last, best, id, cand);
       }
   };
   int stack[64], sp = 0, node = 0;
+  g_segs += 1;
   for (;;) {
+    g_visits += 1;
     const BvhNode& nd = S.t.nodes[node];
     float tn[2], tf[2];
     bool hit[2];
     for (int c = 0; c < 2; ++c) {
-      const float x0 = (nd.x[c] - ex) * rx, x1 = (nd.x[2 + c] - ex) * rx;
-      const float y0 = (nd.y[c] - ey) * ry, y1 = (nd.y[2 + c] - ey) * ry;
-      const float z0 = (nd.z[c] - ez) * rz, z1 = (nd.z[2 + c] - ez) * rz;
+      const float x0 = (nd.x[c] - P - ex) * rx, x1 = (nd.x[2 + c] + P - ex) * rx;
+      const float y0 = (nd.y[c] - P - ey) * ry, y1 = (nd.y[2 + c] + P - ey) * ry;
+      const float z0 = (nd.z[c] - P - ez) * rz, z1 = (nd.z[2 + c] + P - ez) * rz;
       tn[c] = std::max({std::min(x0, x1), std::min(y0, y1), std::min(z0, z1)});
       tf[c] = std::min({std::max(x0, x1), std::max(y0, y1), std::max(z0, z1)});
       hit[c] = std::max(tn[c], tmin) <= std::min(tf[c], best.t);
@@ -112,6 +134,7 @@ static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float u
     const int c0 = nd.child[0], c1 = nd.child[1];
     const bool l0 = hit[0] && c0 < 0, l1 = hit[1] && c1 < 0;
     int k1 = 0, k2 = 0;
+    g_leafs += l0 + l1;
     if (l0 | l1) leaf(l0 ? ~c0 : ~c1, k1);
     if (l0 & l1) leaf(~c1, k2);
     if (tr) {
@@ -231,19 +254,29 @@ static double g_leaf_passes = 0, g_exact_passes = 0;
 static double wave_cost(const std::vector<const Trav*>& lanes, double* node_steps) {
   if (lanes.empty()) return 0.0;
   size_t L = 0;
-  for (const Trav* t : lanes) L = std::max(L, t->leaves.size());
-  double c = C_OUT;
+  int mb = 0, ob = 0;
+  for (const Trav* t : lanes) {
+    L = std::max(L, t->leaves.size());
+    mb = std::max(mb, __builtin_popcount(t->big_c));
+    ob |= t->big_c;
+  }
+  auto exact = [](int maxpop, int orm) {
+    return g_exact_mode == 0 ? C_EXACT * maxpop : C_EXACT_B * __builtin_popcount(orm);
+  };
+  double c = C_OUT + (g_big_leaves ? g_big_leaves * C_LEAF + exact(mb, ob) : 0.0);
   for (size_t i = 0; i < L; ++i) {
-    int ml = 0, m1 = 0, m2 = 0;
+    int ml = 0, m1 = 0, m2 = 0, o1 = 0, o2 = 0;
     for (const Trav* t : lanes)
       if (i < t->leaves.size()) {
         ml = std::max<int>(ml, t->leaves[i]);
-        m1 = std::max<int>(m1, t->c1[i]);
-        m2 = std::max<int>(m2, t->c2[i]);
+        m1 = std::max<int>(m1, __builtin_popcount(t->c1[i]));
+        m2 = std::max<int>(m2, __builtin_popcount(t->c2[i]));
+        o1 |= t->c1[i];
+        o2 |= t->c2[i];
       }
-    c += C_NODE + C_LEAF * ml + C_EXACT * (m1 + m2);
+    c += C_NODE + C_LEAF * ml + exact(m1, o1) + exact(m2, o2);
     g_leaf_passes += ml;
-    g_exact_passes += m1 + m2;
+    g_exact_passes += g_exact_mode == 0 ? m1 + m2 : __builtin_popcount(o1) + __builtin_popcount(o2);
   }
   *node_steps += double(L);
   return c;
@@ -356,7 +389,13 @@ int main(int argc, char** argv) {
   S.kind.resize(S.n);
   rt_scene_cover(11, 42, S.sph.data(), S.kind.data(), S.mat.data(), S.n);
   if (std::getenv("BIG")) g_bvh_big_ratio = std::atof(std::getenv("BIG"));
-  bvh_build(S.sph.data(), S.n, &S.t, 4, true);
+  if (std::getenv("PAD")) g_pad = std::atof(std::getenv("PAD"));
+  if (std::getenv("EXACT")) g_exact_mode = std::atoi(std::getenv("EXACT"));
+
+  const int ls = std::getenv("LS") ? std::atoi(std::getenv("LS")) : 4;
+  bvh_build(S.sph.data(), S.n, &S.t, ls, true);
+  set_leaf_costs(ls / 2);
+  g_big_leaves = S.t.n_big_leaves;
   std::printf("tree: %zu nodes, depth %d, big %zu\n", S.t.nodes.size(), S.t.depth, S.t.big.size());
   Ctx C{&S, {}, 1200, spp, 50};
   const double lf[3] = {13, 2, 3}, la[3] = {0, 0, 0}, vup[3] = {0, 1, 0};
@@ -379,8 +418,9 @@ int main(int argc, char** argv) {
                 R.steps / R.iters, g_leaf_passes / R.iters, g_exact_passes / R.iters,
                 C_OUT * R.iters / R.cost, C_NODE * R.steps / R.cost, C_LEAF * g_leaf_passes / R.cost,
                 C_EXACT * g_exact_passes / R.cost);
-    std::printf("  candidates rejected by the t bound: %.3f of %.0f\n", g_rej / g_cand, g_cand);
-    g_rej = g_cand = 0;
+    std::printf("  candidates rejected by the t bound: %.3f of %.0f; per segment: %.2f node visits, %.2f leaves\n",
+                g_rej / g_cand, g_cand, g_visits / g_segs, g_leafs / g_segs);
+    g_rej = g_cand = g_segs = g_visits = g_leafs = 0;
     std::printf("%-22s cost/sample %8.1f  wave-iters/sample %.3f  trav steps/wave-iter %.2f  lane eff %.3f\n",
                 names[v], R.cost / R.samples, R.iters / R.samples * 64, R.steps / R.iters,
                 R.lane_steps / (R.steps * 64));
