@@ -95,6 +95,22 @@ __device__ __forceinline__ float rng_uniform(uint32_t& s) {
   return static_cast<float>(s >> 8) * 0x1p-24f;
 }
 
+// Correctly rounded sqrt, the same bits as sqrtf for every input: for
+// x >= 2^-96 (every normal case here) the hardware v_sqrt_f32 corrected by
+// the residuals of its neighbours -- the sequence the compiler emits for
+// sqrtf, without its denormal scaling and zero/inf class fix-up (a rare
+// branch keeps those for tiny, NaN and negative inputs): 16 -> 9 VALU.
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const int si = __builtin_bit_cast(int, s);
+  const float sd = __builtin_bit_cast(float, si - 1), su = __builtin_bit_cast(float, si + 1);
+  const float rd = fmaf(-sd, s, x), ru = fmaf(-su, s, x);
+  float r = rd <= 0.0f ? sd : s;
+  r = ru > 0.0f ? su : r;
+  return r;
+}
+
 // rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32.
 __device__ __forceinline__ float rng_sym(uint32_t& s) {
   return 2.0f * rng_uniform(s) - 1.0f;
@@ -110,7 +126,7 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
     z = rng_sym(s);
     l2 = fmaf(z, z, fmaf(y, y, x * x));
   } while (!(l2 > 0.0f && l2 <= 1.0f));
-  const float il = 1.0f / sqrtf(l2);   // contract: v * (1/|v|)
+  const float il = 1.0f / sqrt_rn(l2);   // contract: v * (1/|v|)
   x = x * il;
   y = y * il;
   z = z * il;
@@ -358,7 +374,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     // ---- one ray-color level: hit-anything over all bodies ----
     --rem;
     ++segs;
-    const float len = sqrtf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
+    const float len = sqrt_rn(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
     const float il = 1.0f / len;                              // vec3a/unit as d * (1/|d|)
     const float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
@@ -375,7 +391,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           st_blk_lanes += __popcll(ex);
         }
       }
-      const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
+      const float sq = (s == last) ? fabsf(h) : sqrt_rn(disc);
       float t = h - sq;                 // nearer root (hittable.clj:15)
       if (!(t > tmin)) t = h + sq;      // farther root (:16-18)
       if (t > tmin && t < best_t) {     // open interval, strictly closer (:19, raytracing.clj:35-42)
@@ -411,7 +427,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // branch-free acceptance (bitwise predicates: no exec-mask blocks)
       auto consider_tie = [&](float h, float disc, int s) {
         if constexpr (STATS) ++st_blk_lanes;
-        const float sq = (s == last) ? fabsf(h) : sqrtf(disc);
+        const float sq = (s == last) ? fabsf(h) : sqrt_rn(disc);
         const float tn = h - sq;
         const float t = tn > tmin ? tn : h + sq;
         const bool acc = (t > tmin) & ((t < best_t) | ((t == best_t) & (s < best)));
@@ -790,7 +806,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const float ri = front ? m.x : m.w;   // 1/eta (host-divided) : eta
         const float un = fmaf(uz, nz, fmaf(uy, ny, ux * nx));
         const float cosv = fminf(-un, 1.0f);
-        const float sinv = sqrtf(fmaf(-cosv, cosv, 1.0f));
+        const float sinv = sqrt_rn(fmaf(-cosv, cosv, 1.0f));
         bool refl = !(ri * sinv <= 1.0f);
         if (!refl && !a.realm) {   // (realm: no Schlick term, no draw; realm/raytracing.clj:158-177)
           const float xi = rng_uniform(st);  // drawn only when refraction is possible
@@ -810,7 +826,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           const float qx = fmaf(nx, cosv, ux) * ri;
           const float qy = fmaf(ny, cosv, uy) * ri;
           const float qz = fmaf(nz, cosv, uz) * ri;
-          const float par = -sqrtf(fabsf(1.0f - fmaf(qz, qz, fmaf(qy, qy, qx * qx))));
+          const float par = -sqrt_rn(fabsf(1.0f - fmaf(qz, qz, fmaf(qy, qy, qx * qx))));
           dx = fmaf(nx, par, qx);
           dy = fmaf(ny, par, qy);
           dz = fmaf(nz, par, qz);
