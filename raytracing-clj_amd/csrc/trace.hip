@@ -111,9 +111,21 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   return r;
 }
 
-// rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32.
+// xi - 0.5 (compute-pixel's jitter, raytracing.clj:145-146), exact in fp32
+__device__ __forceinline__ float rng_centered(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return fmaf(static_cast<float>(s >> 8), 0x1p-24f, -0.5f);
+}
+
+// rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32, so one fma
+// of the 24-bit integer gives the same bits as the mirror's 2*xi - 1.
 __device__ __forceinline__ float rng_sym(uint32_t& s) {
-  return 2.0f * rng_uniform(s) - 1.0f;
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return fmaf(static_cast<float>(s >> 8), 0x1p-23f, -1.0f);
 }
 
 // vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
@@ -337,8 +349,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
       st = mix32(pkey + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
-      const float fx = static_cast<float>(px) + (rng_uniform(st) - 0.5f);
-      const float fy = static_cast<float>(gy) + (rng_uniform(st) - 0.5f);
+      // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
+      const float fx = static_cast<float>(px) + rng_centered(st);
+      const float fy = static_cast<float>(gy) + rng_centered(st);
       const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
       const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));

@@ -37,7 +37,8 @@ namespace rtclj { extern float g_bvh_big_ratio; }
 static double g_cand = 0, g_rej = 0, g_segs = 0, g_visits = 0, g_leafs = 0;
 static float g_pad = 1.0f;
 static int g_big_leaves = 0;
-static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
+static int g_exact_mode = 0;
+static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
 static double C_EXACT_B = 32;
 
 // VALU wave-instructions per block (from the ISA of the default kernel,
@@ -67,6 +68,7 @@ struct Scene {
 
 // one segment's traversal as the kernel runs it
 struct Trav {
+  int disk_tries = 0, ball_tries = 0;   // rejection-loop trips of this lane's iteration
   int big_c = 0;                 // candidate bitmask of the big bodies (their leaf pass: every segment)
   std::vector<uint8_t> leaves;   // per visit: leaves entered (0-2)
   std::vector<uint8_t> c1, c2;   // per visit: candidate bitmasks of the first / second leaf
@@ -188,7 +190,7 @@ static bool step(const Ctx& C, Path& p, int px, int py, Trav& tr) {
     float s[3], o[3];
     for (int a = 0; a < 3; ++a) s[a] = C.cam.p00[a] + C.cam.du[a] * fx + C.cam.dv[a] * fy;
     float qx, qy;
-    do { qx = p.rng.sym(); qy = p.rng.sym(); } while (!(qx * qx + qy * qy < 1.0f));
+    do { qx = p.rng.sym(); qy = p.rng.sym(); ++tr.disk_tries; } while (!(qx * qx + qy * qy < 1.0f));
     for (int a = 0; a < 3; ++a) o[a] = C.cam.center[a] + C.cam.disk_u[a] * qx + C.cam.disk_v[a] * qy;
     for (int a = 0; a < 3; ++a) { p.o[a] = o[a]; p.d[a] = s[a] - o[a]; }
     p.rem = C.depth;
@@ -212,7 +214,7 @@ static bool step(const Ctx& C, Path& p, int px, int py, Trav& tr) {
   const float* m = &S.mat[4 * h.body];
   if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
     float q[3], l2;
-    do { q[0] = p.rng.sym(); q[1] = p.rng.sym(); q[2] = p.rng.sym(); l2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2]; }
+    do { q[0] = p.rng.sym(); q[1] = p.rng.sym(); q[2] = p.rng.sym(); l2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2]; ++tr.ball_tries; }
     while (!(l2 > 0.0f && l2 <= 1.0f));
     const float il = 1.0f / std::sqrt(l2);
     for (float& x : q) x *= il;
@@ -254,8 +256,11 @@ static double g_leaf_passes = 0, g_exact_passes = 0;
 static double wave_cost(const std::vector<const Trav*>& lanes, double* node_steps) {
   if (lanes.empty()) return 0.0;
   size_t L = 0;
-  int mb = 0, ob = 0;
+  int mb = 0, ob = 0, md = 0, mball = 0, mboth = 0;
   for (const Trav* t : lanes) {
+    md = std::max(md, t->disk_tries);
+    mball = std::max(mball, t->ball_tries);
+    mboth = std::max(mboth, std::max(t->disk_tries, t->ball_tries));
     L = std::max(L, t->leaves.size());
     mb = std::max(mb, __builtin_popcount(t->big_c));
     ob |= t->big_c;
@@ -263,6 +268,9 @@ static double wave_cost(const std::vector<const Trav*>& lanes, double* node_step
   auto exact = [](int maxpop, int orm) {
     return g_exact_mode == 0 ? C_EXACT * maxpop : C_EXACT_B * __builtin_popcount(orm);
   };
+  g_disk += md;
+  g_ball += mball;
+  g_both += mboth;
   double c = C_OUT + (g_big_leaves ? g_big_leaves * C_LEAF + exact(mb, ob) : 0.0);
   for (size_t i = 0; i < L; ++i) {
     int ml = 0, m1 = 0, m2 = 0, o1 = 0, o2 = 0;
@@ -418,6 +426,9 @@ int main(int argc, char** argv) {
                 R.steps / R.iters, g_leaf_passes / R.iters, g_exact_passes / R.iters,
                 C_OUT * R.iters / R.cost, C_NODE * R.steps / R.cost, C_LEAF * g_leaf_passes / R.cost,
                 C_EXACT * g_exact_passes / R.cost);
+    std::printf("  rejection loops per wave-iter: disk %.2f ball %.2f (one merged loop: %.2f)\n",
+                g_disk / R.iters, g_ball / R.iters, g_both / R.iters);
+    g_disk = g_ball = g_both = 0;
     std::printf("  candidates rejected by the t bound: %.3f of %.0f; per segment: %.2f node visits, %.2f leaves\n",
                 g_rej / g_cand, g_cand, g_visits / g_segs, g_leafs / g_segs);
     g_rej = g_cand = g_segs = g_visits = g_leafs = 0;
