@@ -140,8 +140,15 @@ def bvh_counters(ds, cam, p, out, counters, sh, variant):
         segs = float(counters[0].item())
     finally:
         lib.rt_set_variant(old)
+    wi = max(dbg[0], 1)
     return {"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs, "exact_tests": dbg[4] / segs,
-            "stats_variant": sv}
+            "stats_variant": sv,
+            # wave-level events per wave loop iteration (what the VALU issues for)
+            "per_wave_iter": {"wave_iters_per_sample": wi / max(float(counters[1].item()), 1.0),
+                              "lanes_active": dbg[1] / wi / 64.0, "trav_steps": dbg[6] / wi,
+                              "trav_lane_eff": dbg[7] / max(dbg[6], 1) / 64.0,
+                              "leaf_passes": dbg[12] / wi, "exact_passes": dbg[13] / wi,
+                              "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi}}
 
 
 def _pmc_avg(passes, counters):

@@ -219,7 +219,8 @@ int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int* out4);
  * per stripe in sample order after the pool.  -3: one pool of 8 x 8 pixels
  * per workgroup, shared by its 4 waves.  Pools exist for the BVH variants 11,
  * 13, 16-19; the scratch is per scene and stream, about 12 bytes per sample
- * up to 2 GiB a launch, more launches beyond.  0 = automatic: -3 where the
+ * up to 1/8 of the device memory a launch (RTCLJ_POOL_BYTES overrides), more
+ * launches beyond.  0 = automatic: -3 where the
  * variant has it, else by frame size.  Changes the launch shape, never the
  * result.  Returns the previous value. */
 int rt_set_lanes_per_pixel(int lpp);
@@ -245,8 +246,9 @@ int rt_set_schedule(int mode);
  * [6] BVH wave-level traversal iterations, [7] lanes active in them,
  * [8..11] shader clocks per wave spent in camera sampling, hit search,
  * shading, accumulation (s_memtime; summed over waves), [12] BVH
- * wave-level leaf passes, [13] wave-level exact-test passes.  Synchronises
- * the device. */
+ * wave-level leaf passes, [13] wave-level exact-test passes, [14] / [15]
+ * wave-level trips of the random-unit-vec3 / defocus-disk rejection loops.
+ * Synchronises the device. */
 int rt_debug_stats(uint64_t* out16);
 
 /* Diagnostic wave timeline of variant 3's last launches: n_waves x

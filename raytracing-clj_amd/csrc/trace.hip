@@ -130,9 +130,17 @@ __device__ __forceinline__ float rng_sym(uint32_t& s) {
 
 // vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
 // 0 < |v|^2 <= 1 (1e-160 underflows to 0 in fp32), then v / |v|.
-__device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z) {
+// stats builds: count one event per wave (by its first active lane)
+__device__ __forceinline__ void wave_event(uint64_t& c) {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  if ((threadIdx.x & 63) == static_cast<unsigned>(__ffsll(static_cast<long long>(ex)) - 1)) ++c;
+}
+
+template <bool STATS = false>
+__device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z, uint64_t* trips = nullptr) {
   float l2;
   do {
+    if constexpr (STATS) wave_event(*trips);
     x = rng_sym(s);
     y = rng_sym(s);
     z = rng_sym(s);
@@ -219,6 +227,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
+  uint64_t st_ball = 0, st_disk = 0;          // wave-level rejection-loop trips (random-unit, disk)
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if (STATS || a.tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
@@ -359,6 +368,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
         float qx, qy;
         do {
+          if constexpr (STATS) wave_event(st_disk);
           qx = rng_sym(st);
           qy = rng_sym(st);
         } while (!(fmaf(qy, qy, qx * qx) < 1.0f));
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // the segment for these lanes): a wave loops the rejection sampler
         // once for both kinds
         float qx, qy, qz;
-        random_unit(st, qx, qy, qz);
+        random_unit<STATS>(st, qx, qy, qz, &st_ball);
         if (kind == RT_LAMBERTIAN) {
           // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
           float sx = qx + nx, sy = qy + ny, sz = qz + nz;
@@ -1005,6 +1015,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[12], static_cast<unsigned long long>(st_leafw));
       atomicAdd(&a.dbg[13], static_cast<unsigned long long>(st_consw));
     }
+    if (a.dbg && (st_ball | st_disk)) {
+      atomicAdd(&a.dbg[14], static_cast<unsigned long long>(st_ball));
+      atomicAdd(&a.dbg[15], static_cast<unsigned long long>(st_disk));
+    }
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
@@ -1143,12 +1157,19 @@ static const Variant& variant_table(int v) {
 }
 #undef RT_K
 static int g_lpp = 0;  // 0 = automatic, -1 / -2 = sample pool 4 x 4 / 8 x 8
-// sample-pool scratch per launch (beyond it: more rounds); RTCLJ_POOL_BYTES
-// lowers it (tests: many rounds on a small frame)
+// sample-pool scratch per launch (beyond it: more rounds).  A workgroup's pool
+// should hold ~100+ samples per pixel: shorter pools end more often, and every
+// end idles lanes until the pool's last path is done (C2 at 500 spp: 20-sample
+// rounds 8150 Msamples/s, 172-sample rounds 11380).  Default: 1/8 of the
+// device's memory (36 GB on an MI355X), at most half of what is free, at
+// least 2 GB; RTCLJ_POOL_BYTES overrides it (tests: many rounds, small frame).
 static size_t pool_bytes() {
   const char* e = std::getenv("RTCLJ_POOL_BYTES");
   const long long v = e ? std::atoll(e) : 0;
-  return v > 0 ? static_cast<size_t>(v) : (size_t(2) << 30);
+  if (v > 0) return static_cast<size_t>(v);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return size_t(2) << 30;
+  return std::max(size_t(2) << 30, std::min(total_b / 8, free_b / 2));
 }
 
 // Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
@@ -1206,6 +1227,7 @@ struct Schedule {
   int* order = nullptr;
   float* scratch = nullptr;   // the sample pool's per-wave sample colours
   size_t scratch_bytes = 0;
+  size_t pool_budget = 0;     // scratch budget (pool_bytes(), fixed at the stream's first pool launch)
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
@@ -1523,10 +1545,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // pool scratch: per wave 16 / 64 pixels x chunk samples x rgb, chunk = spp
     // up to pool_bytes() for the whole launch (more rounds beyond that), + the
     // 64 lanes' sums between rounds (6 floats)
+    if (sch->pool_budget == 0) sch->pool_budget = pool_bytes();   // once per scene and stream
     const size_t waves = static_cast<size_t>(n_tiles) * 4;
     const size_t per_sample = waves * (lpp == -2 ? 64 : 16) * 3 * sizeof(float);   // (-3: 64 per 4 waves)
     const int chunk = static_cast<int>(std::max<size_t>(
-        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), pool_bytes() / per_sample, 16384})));
+        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), sch->pool_budget / per_sample, 16384})));
     const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
     if (sch->scratch_bytes < need) {   // grow (this stream's kernels may still use the old one)
       HIP_TRY(hipStreamSynchronize(stream));

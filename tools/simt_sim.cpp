@@ -37,8 +37,8 @@ namespace rtclj { extern float g_bvh_big_ratio; }
 static double g_cand = 0, g_rej = 0, g_segs = 0, g_visits = 0, g_leafs = 0;
 static float g_pad = 1.0f;
 static int g_big_leaves = 0;
-static int g_exact_mode = 0;
-static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
+static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
+static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
 static double C_EXACT_B = 32;
 
 // VALU wave-instructions per block (from the ISA of the default kernel,
