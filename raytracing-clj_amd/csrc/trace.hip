@@ -1163,10 +1163,12 @@ static int g_lpp = 0;  // 0 = automatic, -1 / -2 = sample pool 4 x 4 / 8 x 8
 // rounds 8150 Msamples/s, 172-sample rounds 11380).  Default: 1/8 of the
 // device's memory (36 GB on an MI355X), at most half of what is free, at
 // least 2 GB; RTCLJ_POOL_BYTES overrides it (tests: many rounds, small frame).
-static size_t pool_bytes() {
+static size_t pool_bytes_env() {
   const char* e = std::getenv("RTCLJ_POOL_BYTES");
   const long long v = e ? std::atoll(e) : 0;
-  if (v > 0) return static_cast<size_t>(v);
+  return v > 0 ? static_cast<size_t>(v) : 0;
+}
+static size_t pool_bytes_default() {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return size_t(2) << 30;
   return std::max(size_t(2) << 30, std::min(total_b / 8, free_b / 2));
@@ -1227,7 +1229,7 @@ struct Schedule {
   int* order = nullptr;
   float* scratch = nullptr;   // the sample pool's per-wave sample colours
   size_t scratch_bytes = 0;
-  size_t pool_budget = 0;     // scratch budget (pool_bytes(), fixed at the stream's first pool launch)
+  size_t pool_budget = 0;     // default scratch budget (pool_bytes_default(), at the stream's first pool launch)
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
@@ -1543,13 +1545,18 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   if (lpp < 0) {
     // pool scratch: per wave 16 / 64 pixels x chunk samples x rgb, chunk = spp
-    // up to pool_bytes() for the whole launch (more rounds beyond that), + the
+    // up to the scratch budget for the whole launch (more rounds beyond that), + the
     // 64 lanes' sums between rounds (6 floats)
-    if (sch->pool_budget == 0) sch->pool_budget = pool_bytes();   // once per scene and stream
+    // RTCLJ_POOL_BYTES per launch; the device default once per scene and stream
+    size_t budget = pool_bytes_env();
+    if (budget == 0) {
+      if (sch->pool_budget == 0) sch->pool_budget = pool_bytes_default();
+      budget = sch->pool_budget;
+    }
     const size_t waves = static_cast<size_t>(n_tiles) * 4;
     const size_t per_sample = waves * (lpp == -2 ? 64 : 16) * 3 * sizeof(float);   // (-3: 64 per 4 waves)
     const int chunk = static_cast<int>(std::max<size_t>(
-        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), sch->pool_budget / per_sample, 16384})));
+        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), budget / per_sample, 16384})));
     const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
     if (sch->scratch_bytes < need) {   // grow (this stream's kernels may still use the old one)
       HIP_TRY(hipStreamSynchronize(stream));

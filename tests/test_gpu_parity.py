@@ -354,6 +354,41 @@ def test_bvh_small_scenes(gpu_lib, n):
     assert np.array_equal(out[5], ref)
 
 
+@pytest.mark.parametrize("n_big", [1, 3, 4, 5, 9, 12])
+def test_bvh_big_bodies(gpu_lib, n_big):
+    """Bodies > 4x the median radius leave the tree (up to 8 of them, largest
+    first; bvh.cpp) and are tested as packed leaves of their own before every
+    traversal: 1, 2 or 3 such leaves for 2-, 4- and 8-body trees, ties in
+    radius, the rest staying in the tree -- all == the scan and the mirror."""
+    from rtclj import raytracing as R
+    from rtclj._lib import lib
+    rng = np.random.default_rng(100 + n_big)
+    n = 60 + n_big
+    sph = np.zeros((n, 4), np.float32)
+    sph[:, 0] = rng.uniform(-4, 4, n)
+    sph[:, 1] = rng.uniform(0, 1, n)
+    sph[:, 2] = rng.uniform(-8, -1, n)
+    sph[:, 3] = 0.2
+    big = rng.choice(n, n_big, replace=False)
+    sph[big, 3] = rng.choice([1.0, 1.5], n_big)          # ties among the big radii
+    sph[big[0]] = (0.0, -100.5, -1.0, 100.0)             # a ground
+    kind = rng.integers(0, 3, n).astype(np.int32)
+    mat = np.column_stack([rng.uniform(0, 1, (n, 3)), np.where(kind == 2, 1.5, 0.3)]).astype(np.float32)
+    sc = R.Scene(sph, kind, mat)
+    cam = R.camera(64, 36, **R.REFERENCE_CAMERA)
+    out = {}
+    for v in (5, 11, 16, 18):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 64, 36, spp=8, max_depth=20, seed=9)
+        finally:
+            lib.rt_set_variant(old)
+    for v in (11, 16, 18):
+        assert np.array_equal(out[5], out[v]), v
+    ref, _, _ = _mirror(sc, cam, 64, 36, 8, 20, seed=9)
+    assert np.array_equal(out[5], ref)
+
+
 @pytest.mark.parametrize("variant", [0, 11, 16, 18])
 def test_bvh_large_scene_falls_back(gpu_lib, variant):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
