@@ -76,7 +76,7 @@ struct alignas(16) KArgs {
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
   unsigned* tile_cost;     // nullable: per tile, the longest of its waves' durations (s_memrealtime ticks)
-  float* pool_scratch;     // sample pool (LPP 0): per wave 16 pixels x pool_chunk samples x rgb
+  float* pool_scratch;     // sample pool (LPP < 0): per pool, [pixel][pool_chunk samples][rgb], then the lanes' sums
   int pool_chunk;          // samples per pixel per pool round (one launch per round)
   int pool_c0;             // this launch's round starts at sample pool_c0 of each pixel
   int spp, sample_begin, max_depth;
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
     if (POOL) {
       if (done) {
-        float* d = scr + ((k - c0) * PPX + q) * 3;
+        float* d = scr + (q * a.pool_chunk + (k - c0)) * 3;   // [pixel][sample][rgb]
         d[0] = cr;
         d[1] = cg;
         d[2] = cb;
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const int b = stripe_begin(sp, a.spp, P), e = stripe_begin(sp + 1, a.spp, P);
         const int sb = max(b, c0), se = min(e, c0 + cn);
         for (int s = sb; s < se; ++s) {
-          const float* d = scr + ((s - c0) * PPX + fp) * 3;
+          const float* d = scr + (fp * a.pool_chunk + (s - c0)) * 3;
           accr += d[0];
           accg += d[1];
           accb += d[2];
