@@ -1,8 +1,6 @@
 set -e
-mkdir -p gpurun_out/pool
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pool/pytest.log 2>&1
-tail -1 gpurun_out/pool/pytest.log
-for wl in c1 c2; do
-  timeout -k 10 300 python -u bench.py --workload $wl --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/pool/$wl.json 2> gpurun_out/pool/$wl.err
-  python -c "import json; d=json.load(open('gpurun_out/pool/$wl.json')); print('$wl', round(d['value']), round(d['kernel_ms_avg'],2), json.dumps(d['bvh_per_segment']['per_wave_iter']))"
-done
+mkdir -p gpurun_out/c4
+timeout -k 10 600 python -u bench.py --workload c4 --steps 1 --warmup 1 --cpu-baseline off > gpurun_out/c4/c4.json 2> gpurun_out/c4/c4.err
+python -c "import json; d=json.load(open('gpurun_out/c4/c4.json')); print('c4', round(d['value']), round(d['kernel_ms_avg'],1), d['config'], d['occupancy']['lds_bytes_per_wg'])"
+timeout -k 10 300 python -u bench.py --workload c2 --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/c4/c2.json 2> gpurun_out/c4/c2.err
+python -c "import json; d=json.load(open('gpurun_out/c4/c2.json')); print('c2', round(d['value']), round(d['kernel_ms_avg'],1))"
