@@ -518,8 +518,17 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           dd[2 * q + 1] = disc.y;
           ii[2 * q] = id.x;
           ii[2 * q + 1] = id.y;
-          m |= static_cast<unsigned>(fminf(disc.x, fmaxf(h.x, -c.x)) >= 0.0f) << (2 * q);
-          m |= static_cast<unsigned>(fminf(disc.y, fmaxf(h.y, -c.y)) >= 0.0f) << (2 * q + 1);
+          // candidate: disc >= 0 and not (h < 0 and c >= 0), read from the sign
+          // bits (disc | (h & ~c)): the same bodies as the scan's test except
+          // c = -0 or h = -0 or NaN operands, whose roots the exact test
+          // rejects anyway (t <= t-min or NaN)
+          // (halves copied to scalars first: __builtin_bit_cast of an
+          // ext_vector element read the .x half for .y here)
+          const float d0 = disc.x, d1 = disc.y, h0 = h.x, h1 = h.y, k0 = c.x, k1 = c.y;
+          const unsigned nx = __float_as_uint(d0) | (__float_as_uint(h0) & ~__float_as_uint(k0));
+          const unsigned ny = __float_as_uint(d1) | (__float_as_uint(h1) & ~__float_as_uint(k1));
+          m |= ((~nx) >> 31) << (2 * q);
+          m |= ((~ny) >> 31) << (2 * q + 1);
         }
         // one pass of the exact test per candidate: the wave runs it as often
         // as its lane with the most candidates needs (not once per body)
