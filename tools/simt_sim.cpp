@@ -39,6 +39,7 @@ static float g_pad = 1.0f;
 static int g_big_leaves = 0;
 static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
 static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
+static double g_abs = 0;   // wave iterations with a metal absorption
 static double C_EXACT_B = 32;
 
 // VALU wave-instructions per block (from the ISA of the default kernel,
@@ -69,6 +70,7 @@ struct Scene {
 // one segment's traversal as the kernel runs it
 struct Trav {
   int disk_tries = 0, ball_tries = 0;   // rejection-loop trips of this lane's iteration
+  int absorbed = 0;                     // a metal scatter went below the surface
   int big_c = 0;                 // candidate bitmask of the big bodies (their leaf pass: every segment)
   std::vector<uint8_t> leaves;   // per visit: leaves entered (0-2)
   std::vector<uint8_t> c1, c2;   // per visit: candidate bitmasks of the first / second leaf
@@ -224,7 +226,10 @@ static bool step(const Ctx& C, Path& p, int px, int py, Trav& tr) {
       const float k2 = 2.0f * (p.d[0] * n[0] + p.d[1] * n[1] + p.d[2] * n[2]);
       float r[3];
       for (int a = 0; a < 3; ++a) r[a] = p.d[a] - n[a] * k2 + m[3] * q[a];
-      if (!(r[0] * n[0] + r[1] * n[1] + r[2] * n[2] > 0.0f)) return true;
+      if (!(r[0] * n[0] + r[1] * n[1] + r[2] * n[2] > 0.0f)) {
+        tr.absorbed = 1;
+        return true;
+      }
       for (int a = 0; a < 3; ++a) p.d[a] = r[a];
     }
   } else {
@@ -256,11 +261,12 @@ static double g_leaf_passes = 0, g_exact_passes = 0;
 static double wave_cost(const std::vector<const Trav*>& lanes, double* node_steps) {
   if (lanes.empty()) return 0.0;
   size_t L = 0;
-  int mb = 0, ob = 0, md = 0, mball = 0, mboth = 0;
+  int mb = 0, ob = 0, md = 0, mball = 0, mboth = 0, anyabs = 0;
   for (const Trav* t : lanes) {
     md = std::max(md, t->disk_tries);
     mball = std::max(mball, t->ball_tries);
     mboth = std::max(mboth, std::max(t->disk_tries, t->ball_tries));
+    anyabs |= t->absorbed;
     L = std::max(L, t->leaves.size());
     mb = std::max(mb, __builtin_popcount(t->big_c));
     ob |= t->big_c;
@@ -268,6 +274,7 @@ static double wave_cost(const std::vector<const Trav*>& lanes, double* node_step
   auto exact = [](int maxpop, int orm) {
     return g_exact_mode == 0 ? C_EXACT * maxpop : C_EXACT_B * __builtin_popcount(orm);
   };
+  g_abs += anyabs;
   g_disk += md;
   g_ball += mball;
   g_both += mboth;
@@ -426,9 +433,9 @@ int main(int argc, char** argv) {
                 R.steps / R.iters, g_leaf_passes / R.iters, g_exact_passes / R.iters,
                 C_OUT * R.iters / R.cost, C_NODE * R.steps / R.cost, C_LEAF * g_leaf_passes / R.cost,
                 C_EXACT * g_exact_passes / R.cost);
-    std::printf("  rejection loops per wave-iter: disk %.2f ball %.2f (one merged loop: %.2f)\n",
-                g_disk / R.iters, g_ball / R.iters, g_both / R.iters);
-    g_disk = g_ball = g_both = 0;
+    std::printf("  rejection loops per wave-iter: disk %.2f ball %.2f (one merged loop: %.2f); absorption in %.3f of wave-iters\n",
+                g_disk / R.iters, g_ball / R.iters, g_both / R.iters, g_abs / R.iters);
+    g_disk = g_ball = g_both = g_abs = 0;
     std::printf("  candidates rejected by the t bound: %.3f of %.0f; per segment: %.2f node visits, %.2f leaves\n",
                 g_rej / g_cand, g_cand, g_visits / g_segs, g_leafs / g_segs);
     g_rej = g_cand = g_segs = g_visits = g_leafs = 0;
