@@ -40,6 +40,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "bvh.h"
@@ -245,7 +246,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     __syncthreads();
   }
   // BVH traversal stack: bvh_stack node refs per lane, [entry][lane] (no bank conflicts)
-  unsigned short* s_stack = reinterpret_cast<unsigned short*>(
+  // (u8 entries for the 8-body-leaf traversal, whose trees the host caps at
+  // 256 nodes: with its u16 body indices this keeps a 1025-body scene's
+  // image under the 32 KB that 5 workgroups per CU allow)
+  using StackT = std::conditional_t<SCAN == SCAN_BVHO, unsigned char, unsigned short>;
+  StackT* s_stack = reinterpret_cast<StackT*>(
       reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
 
   // lane -> (pixel, stripe group): a wave owns a TW x TH pixel tile
@@ -463,7 +468,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
                                         : reinterpret_cast<const char*>(a.bvh_blob);
       const KNode* nodes = reinterpret_cast<const KNode*>(base);
       const Pair* pairs = reinterpret_cast<const Pair*>(base + a.bvh_off_pairs);
-      const int2* pidx = reinterpret_cast<const int2*>(base + a.bvh_off_pidx);
+      // body indices: u16 in the 8-body-leaf tree (LDS size), int elsewhere
+      // (an int pair is one read with no unpacking: the 4-body leaf pass is hot)
+      using PidxT = std::conditional_t<SCAN == SCAN_BVHO, ushort2, int2>;
+      const PidxT* pidx = reinterpret_cast<const PidxT*>(base + a.bvh_off_pidx);
       // box tests only cull (conservatively): hardware sqrt / rcp (1 ulp) are
       // far inside the padding.  Node boxes are stored relative to the tree
       // centre c (bvh.cpp), so every slab bound is one fma:
@@ -500,14 +508,20 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           const uint64_t ex = __builtin_amdgcn_read_exec();
           if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_leafw;
         }
-        constexpr int NP = leaf_pairs(SCAN);
+        // an 8-body leaf runs as two 4-body halves, each with its own exact
+        // passes: 4 bodies' (h, disc, index) live at a time, not 8 (103 -> ~90
+        // VGPRs, 4 -> 5 waves per SIMD); the acceptance is order-independent
+        constexpr int NPL = leaf_pairs(SCAN);
+        constexpr int NP = NPL > 2 ? 2 : NPL;   // pairs per half
+#pragma unroll
+        for (int hb = 0; hb < NPL; hb += NP) {
         float hh[2 * NP], dd[2 * NP];
         int ii[2 * NP];
-        unsigned m = 0;   // candidate bodies of the leaf
+        unsigned m = 0;   // candidate bodies of the half
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-          const Pair g = pairs[p + q];
-          const int2 id = pidx[p + q];
+          const Pair g = pairs[p + hb + q];
+          const PidxT id = pidx[p + hb + q];
           const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
           const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
           const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
@@ -548,6 +562,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
             s = k == static_cast<unsigned>(j) ? ii[j] : s;
           }
           consider_tie(h, d, s);
+        }
         }
       };
       // slab test of both children of node nd: entry/exit t and the cull
@@ -669,7 +684,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const bool i0 = hit0 && c0 >= 0, i1 = hit1 && c1 >= 0;
         const bool sw = tn1 < tn0;
         const int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
-        s_stack[sp * 256 + threadIdx.x] = static_cast<unsigned short>(sw ? c0 : c1);
+        s_stack[sp * 256 + threadIdx.x] = static_cast<StackT>(sw ? c0 : c1);
         sp += (i0 && i1) ? 1 : 0;
         if (!(i0 || i1)) {
           if (sp == 0) break;
@@ -1216,7 +1231,7 @@ using namespace rtclj;
 // one BVH on the device: blob = nodes | pairs | pidx (the big bodies' leaves after the tree's)
 struct DTree {
   float4* blob;
-  int blob_f4, off_pairs, off_pidx, big_pair0, n_big_leaves, depth;
+  int blob_f4, off_pairs, off_pidx, big_pair0, n_big_leaves, depth, n_nodes;
   float c[3], r;
 };
 
@@ -1357,11 +1372,17 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     bvh_build(s->sphere, n, &bvh, 2 << k, g_bvh_sah);
     const size_t nb = bvh.nodes.size() * sizeof(BvhNode);
     const size_t pb = bvh.pairs.size() * sizeof(float);
-    const size_t ib = ((bvh.pidx.size() * sizeof(int) + 15) / 16) * 16;
+    // body indices: u16 for the 8-body-leaf tree (RT_MAX_SPHERES < 65535; a
+    // pad's -1 -> 0xffff, never a candidate), int for the others
+    const size_t isz = k == 2 ? sizeof(uint16_t) : sizeof(int);
+    std::vector<uint16_t> pidx16(bvh.pidx.size());
+    for (size_t i = 0; i < pidx16.size(); ++i) pidx16[i] = static_cast<uint16_t>(bvh.pidx[i]);
+    const size_t ib = ((bvh.pidx.size() * isz + 15) / 16) * 16;
     std::vector<char> blob(nb + pb + ib, 0);
     std::memcpy(blob.data(), bvh.nodes.data(), nb);
     std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
-    std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
+    if (k == 2) std::memcpy(blob.data() + nb + pb, pidx16.data(), pidx16.size() * sizeof(uint16_t));
+    else std::memcpy(blob.data() + nb + pb, bvh.pidx.data(), bvh.pidx.size() * sizeof(int));
     DTree& t = d->tree[k];
     t.blob_f4 = static_cast<int>(blob.size() / 16);
     t.off_pairs = static_cast<int>(nb);
@@ -1369,6 +1390,7 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     t.big_pair0 = bvh.big_pair0;
     t.n_big_leaves = bvh.n_big_leaves;
     t.depth = bvh.depth;
+    t.n_nodes = static_cast<int>(bvh.nodes.size());
     for (int j = 0; j < 3; ++j) t.c[j] = bvh.center[j];
     t.r = bvh.radius;
     e = hipMalloc(&t.blob, blob.size());
@@ -1407,19 +1429,26 @@ extern "C" int rt_scene_free(rt_dscene* d) {
   return RT_OK;
 }
 
-static size_t stack_of(const DTree& t) { return static_cast<size_t>(t.depth + 2) * 256 * sizeof(unsigned short); }
-static size_t lds_of(const DTree& t) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t); }
+// traversal stack bytes: u8 entries for the 8-body-leaf tree (tree[2], at
+// most 256 nodes when its variant runs), u16 otherwise
+static size_t stack_of(const DTree& t, int tree) {
+  return static_cast<size_t>(t.depth + 2) * 256 * (tree == 2 ? 1 : 2);
+}
+static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
 
 // selector -> the variant a launch on ds runs
 static int resolve_variant(const rt_dscene& ds, int vsel) {
   // default: 4-body leaves, unless that tree's LDS image limits a CU below
   // the 5 workgroups the registers allow (160 KB / 5) and the 8-body-leaf
   // tree's is smaller (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
-  if (vsel == 0) vsel = (lds_of(ds.tree[1]) > 32 * 1024 && lds_of(ds.tree[2]) < lds_of(ds.tree[1])) ? 18 : 16;
+  if (vsel == 0)
+    vsel = (lds_of(ds.tree[1], 1) > 32 * 1024 && ds.tree[2].n_nodes <= 256 &&
+            lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
+  if ((vsel == 18 || vsel == 19) && ds.tree[2].n_nodes > 256) vsel -= 2;   // u8 stack: 256 nodes at most
   if (vsel >= 11) {
     const DTree& t = ds.tree[variant_tree(vsel)];
     if (t.depth + 2 > kBvhStack) return 5;                       // tree too deep for the stack
-    if (vsel != 12 && lds_of(t) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
+    if (vsel != 12 && lds_of(t, variant_tree(vsel)) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
     if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
   }
   return vsel;
@@ -1441,7 +1470,7 @@ extern "C" int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int*
   const int lpp = choose_lpp(p->width, rows, p->spp, v);
   const void* fn = v.fn[fn_slot(lpp)];
   if (!fn) return set_error(RT_E_ARG, "rt_launch_occupancy: no launch shape");
-  const size_t lds = vsel >= 11 ? (v.lds ? lds_of(tr) : stack_of(tr))
+  const size_t lds = vsel >= 11 ? (v.lds ? lds_of(tr, variant_tree(vsel)) : stack_of(tr, variant_tree(vsel)))
                                 : (v.lds ? static_cast<size_t>(ds->n_pad) * sizeof(float4) : 0);
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
@@ -1496,8 +1525,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   HIP_TRY(hipSetDevice(ds->device));
   const int vsel = resolve_variant(*ds, g_variant);
   const DTree& tr = ds->tree[variant_tree(vsel)];
-  const size_t stack_bytes = stack_of(tr);
-  const size_t bvh_lds = lds_of(tr);
+  const size_t stack_bytes = stack_of(tr, variant_tree(vsel));
+  const size_t bvh_lds = lds_of(tr, variant_tree(vsel));
   const Variant& v = variant_table(vsel);
   const bool is_bvh = vsel >= 11;
   a.bvh_blob = tr.blob;
