@@ -178,7 +178,7 @@ def pmc_traffic():
     return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(PMC_DEFAULT.relative_to(ROOT))
 
 
-def occupancy(ds, p, n_simd=1024, n_xcd=8):
+def occupancy(ds, p, with_pmc, n_simd=1024, n_xcd=8):
     """Resident waves per SIMD: the launch's limit (HIP occupancy query with its
     dynamic LDS; VGPRs) and the measured mean over the timed kernel's launches
     from the committed PMC pass (SQ_WAVE_CYCLES in 4-cycle units summed over
@@ -188,7 +188,7 @@ def occupancy(ds, p, n_simd=1024, n_xcd=8):
     limit = min(8.0, o[0] * 4 / 4.0)   # 256-thread workgroups per CU x 4 waves / 4 SIMDs
     res = {"limit_waves_per_simd": limit, "workgroups_per_cu": o[0], "vgprs": o[1], "lds_bytes_per_wg": o[2],
            "lanes_per_pixel_shape": o[3], "hw_max_waves_per_simd": 8}
-    v = _pmc_avg(("waves",), ("SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"))
+    v = _pmc_avg(("waves",), ("SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")) if with_pmc else None
     if v is not None:
         mean = v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
         res.update({"mean_waves_per_simd": mean, "frac_of_limit": mean / limit, "frac_of_hw_max": mean / 8.0,
@@ -309,7 +309,10 @@ def main():
     segs_total, samples_total = tot.tolist()
     bvh = (bvh_counters(ds, cam, p, out, counters, sh, a.variant)
            if rank == 0 and lib.rt_resolve_variant(ds) in BVH_STATS else None)
-    occ = occupancy(ds, p) if rank == 0 else None
+    # the committed PMC passes were taken on C1's default launch: only that
+    # workload's line quotes them
+    pmc_ok = a.workload == "c1" and not a.spp and a.variant == 0 and a.lpp == 0 and a.scaling == "weak"
+    occ = occupancy(ds, p, pmc_ok) if rank == 0 else None
     lib.rt_scene_free(ds)
 
     if rank == 0:
@@ -334,7 +337,7 @@ def main():
         tflops = launch_segs * per_seg / (kern_avg_ms * 1e-3) / 1e12
         hbm_bytes = rows * W * 12 + len(scene) * 32
         gbs = hbm_bytes / (kern_avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic() if pmc_ok else (None, "no committed PMC pass for this workload")
         res = {
             "metric": METRIC, "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -356,7 +359,7 @@ def main():
             "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
-            "valu": pmc_valu(),
+            "valu": pmc_valu() if pmc_ok else None,
             "occupancy": occ,
             "bvh_per_segment": bvh,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
