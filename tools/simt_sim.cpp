@@ -37,6 +37,7 @@ namespace rtclj { extern float g_bvh_big_ratio; }
 static double g_cand = 0, g_rej = 0, g_segs = 0, g_visits = 0, g_leafs = 0;
 static float g_pad = 1.0f;
 static int g_big_leaves = 0;
+static int g_tile_h = 8;      // workgroup pool: 8 x g_tile_h pixels (TILEH)
 static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
 static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
 static double g_abs = 0;   // wave iterations with a metal absorption
@@ -301,14 +302,14 @@ struct Result { double cost = 0, iters = 0, steps = 0, samples = 0, lane_steps =
 
 // one workgroup tile (8x8 pixels at (tx, ty)) under a policy
 static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Result& R) {
-  const int npx = 64, pool = npx * C.spp;
+  const int npx = 64 * g_tile_h / 8, pool = npx * C.spp;   // 8 x g_tile_h pixels
   std::vector<Path> lanes(256);
   int next = 0;
   for (int l = 0; l < 256; ++l) lanes[l].j = next < pool ? next++ : -1;
   auto pixel = [&](int j, int& px, int& py) {
     const int q = j / C.spp;
     px = tx * 8 + q % 8;
-    py = ty * 8 + q / 8;
+    py = ty * g_tile_h + q / 8;
   };
   R.samples += pool;
   if (policy == 0) {
@@ -415,7 +416,8 @@ int main(int argc, char** argv) {
   Ctx C{&S, {}, 1200, spp, 50};
   const double lf[3] = {13, 2, 3}, la[3] = {0, 0, 0}, vup[3] = {0, 1, 0};
   rt_camera_setup(1200, 675, 20.0, lf, la, vup, 0.6, 10.0, &C.cam);
-  const int gx = 1200 / 8, gy = (675 + 7) / 8;
+  if (std::getenv("TILEH")) g_tile_h = std::atoi(std::getenv("TILEH"));
+  const int gx = 1200 / 8, gy = (675 + g_tile_h - 1) / g_tile_h;
   std::vector<int> pick;
   uint32_t h = 12345;
   for (int i = 0; i < tiles; ++i) {
