@@ -210,7 +210,9 @@ def pmc_valu(n_simd=1024, n_xcd=8):
     return {"issue_busy": busy, "lanes_active": lanes, "valu_insts": v["SQ_INSTS_VALU"],
             "source": str(PMC_DEFAULT.relative_to(ROOT)),
             "note": "the binding limit: VALU issue slots (a wave64 instruction takes 4 cycles whatever its "
-                    "active lanes); executed-flop frac = issue_busy x lanes_active x (flops per issued "
+                    "active lanes); issue_busy ~1 = every SIMD issues a VALU instruction every 4 cycles "
+                    "(SQ_ACTIVE_INST_VALU counts per wave, so overlapping multi-cycle instructions can read "
+                    "a little above 1); executed-flop frac = issue_busy x lanes_active x (flops per issued "
                     "lane-instruction)"}
 
 
