@@ -389,6 +389,71 @@ def test_bvh_big_bodies(gpu_lib, n_big):
     assert np.array_equal(out[5], ref)
 
 
+def test_bvh_cover16_u8_stack_and_u16_indices(gpu_lib):
+    """C4's scene (cover grid 16, 1025 bodies): the 8-body-leaf traversal
+    (u8 stack, u16 body indices, leaves in two halves; the default here) and
+    the 4-body one == the scan == the mirror."""
+    import ctypes as C
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import check, lib
+    sc = scenes.cover(16)
+    cam = scenes.cover_camera(96, 54)
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    try:
+        assert lib.rt_resolve_variant(ds) == 18
+    finally:
+        lib.rt_scene_free(ds)
+    out = {}
+    for v in (5, 16, 18):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 96, 54, spp=6, max_depth=64, seed=4)
+        finally:
+            lib.rt_set_variant(old)
+    assert np.array_equal(out[5], out[16])
+    assert np.array_equal(out[5], out[18])
+    ref, _, _ = _mirror(sc, cam, 96, 54, 6, 64, seed=4)
+    assert np.array_equal(out[5], ref)
+
+
+def test_bvh_8body_tree_over_256_nodes_uses_4body(gpu_lib):
+    """An 8-body tree with more than 256 nodes cannot use the u8 stack:
+    variant 18 resolves to 16 (or to 12 when that tree misses LDS) -- same
+    bits as the scan."""
+    import ctypes as C
+    from rtclj import raytracing as R
+    from rtclj._lib import check, lib
+    rng = np.random.default_rng(7)
+    n = 2600
+    sph = np.zeros((n, 4), np.float32)
+    sph[:, 0] = rng.uniform(-30, 30, n)
+    sph[:, 1] = rng.uniform(0, 1, n)
+    sph[:, 2] = rng.uniform(-40, -2, n)
+    sph[:, 3] = rng.uniform(0.05, 0.2, n)
+    kind = rng.integers(0, 3, n).astype(np.int32)
+    mat = np.column_stack([rng.uniform(0, 1, (n, 3)), np.where(kind == 2, 1.5, 0.3)]).astype(np.float32)
+    sc = R.Scene(sph, kind, mat)
+    cam = R.camera(64, 36, 40.0, (0, 2, 3), (0, 0, -10), (0, 1, 0), 0.0, 10.0)
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    old = lib.rt_set_variant(18)
+    try:
+        assert lib.rt_resolve_variant(ds) in (16, 12)
+    finally:
+        lib.rt_set_variant(old)
+        lib.rt_scene_free(ds)
+    out = {}
+    for v in (5, 18):
+        old = lib.rt_set_variant(v)
+        try:
+            out[v] = R.render(sc, cam, 64, 36, spp=4, max_depth=10, seed=2)
+        finally:
+            lib.rt_set_variant(old)
+    assert np.array_equal(out[5], out[18])
+
+
 @pytest.mark.parametrize("variant", [0, 11, 16, 18])
 def test_bvh_large_scene_falls_back(gpu_lib, variant):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
