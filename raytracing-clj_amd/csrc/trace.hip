@@ -539,8 +539,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           // (halves copied to scalars first: __builtin_bit_cast of an
           // ext_vector element read the .x half for .y here)
           const float d0 = disc.x, d1 = disc.y, h0 = h.x, h1 = h.y, k0 = c.x, k1 = c.y;
-          const unsigned nx = __float_as_uint(d0) | (__float_as_uint(h0) & ~__float_as_uint(k0));
-          const unsigned ny = __float_as_uint(d1) | (__float_as_uint(h1) & ~__float_as_uint(k1));
+          // one v_bitop3_b32 each: LUT 0xf4 = s0 | (s1 & ~s2)
+          const unsigned nx = __builtin_amdgcn_bitop3_b32(__float_as_uint(d0), __float_as_uint(h0),
+                                                          __float_as_uint(k0), 0xf4);
+          const unsigned ny = __builtin_amdgcn_bitop3_b32(__float_as_uint(d1), __float_as_uint(h1),
+                                                          __float_as_uint(k1), 0xf4);
           m |= ((~nx) >> 31) << (2 * q);
           m |= ((~ny) >> 31) << (2 * q + 1);
         }
@@ -657,7 +660,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           }
         }
       } else {
-      int node = 0, sp = 0;
+      int node = 0;
+      // the stack top as a pointer into the [entry][lane] stack: one add per
+      // push / pop instead of index arithmetic
+      StackT* const stk0 = s_stack + threadIdx.x;
+      StackT* top = stk0;
       for (;;) {
         if constexpr (STATS) {
           ++st_sph;
@@ -684,12 +691,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const bool i0 = hit0 && c0 >= 0, i1 = hit1 && c1 >= 0;
         const bool sw = tn1 < tn0;
         const int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
-        s_stack[sp * 256 + threadIdx.x] = static_cast<StackT>(sw ? c0 : c1);
-        sp += (i0 && i1) ? 1 : 0;
+        *top = static_cast<StackT>(sw ? c0 : c1);
+        top += (i0 && i1) ? 256 : 0;
         if (!(i0 || i1)) {
-          if (sp == 0) break;
-          --sp;
-          node = s_stack[sp * 256 + threadIdx.x];
+          if (top == stk0) break;
+          top -= 256;
+          node = *top;
         } else {
           node = nxt;
         }
