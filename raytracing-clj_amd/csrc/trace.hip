@@ -575,7 +575,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // same fma on the same operands -- no min/max orders them)
       auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
         // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
-        const char* nb = reinterpret_cast<const char*>(nodes) + __umul24(static_cast<unsigned>(node), 80u);
+        // the 4-body tree's inner-child refs are byte offsets (node * 80,
+        // written by rt_scene_upload): no multiply per step
+        const char* nb = reinterpret_cast<const char*>(nodes) +
+                         (SCAN == SCAN_BVHQ ? static_cast<unsigned>(node) : __umul24(static_cast<unsigned>(node), 80u));
         const f2* ax = reinterpret_cast<const f2*>(nb + offx);
         const f2* ay = reinterpret_cast<const f2*>(nb + offy);
         const f2* az = reinterpret_cast<const f2*>(nb + offz);
@@ -1386,6 +1389,10 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     for (size_t i = 0; i < pidx16.size(); ++i) pidx16[i] = static_cast<uint16_t>(bvh.pidx[i]);
     const size_t ib = ((bvh.pidx.size() * isz + 15) / 16) * 16;
     std::vector<char> blob(nb + pb + ib, 0);
+    if (k == 1)   // 4-body tree: inner-child refs as byte offsets (< 65536 while it fits LDS: u16 stack)
+      for (BvhNode& nd : bvh.nodes)
+        for (int& c : nd.child)
+          if (c >= 0) c *= static_cast<int>(sizeof(BvhNode));
     std::memcpy(blob.data(), bvh.nodes.data(), nb);
     std::memcpy(blob.data() + nb, bvh.pairs.data(), pb);
     if (k == 2) std::memcpy(blob.data() + nb + pb, pidx16.data(), pidx16.size() * sizeof(uint16_t));
@@ -1452,6 +1459,7 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
     vsel = (lds_of(ds.tree[1], 1) > 32 * 1024 && ds.tree[2].n_nodes <= 256 &&
             lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
   if ((vsel == 18 || vsel == 19) && ds.tree[2].n_nodes > 256) vsel -= 2;   // u8 stack: 256 nodes at most
+  if ((vsel == 16 || vsel == 17) && ds.tree[1].n_nodes * 80 > 65535) vsel = 12;   // u16 stack of byte offsets
   if (vsel >= 11) {
     const DTree& t = ds.tree[variant_tree(vsel)];
     if (t.depth + 2 > kBvhStack) return 5;                       // tree too deep for the stack
