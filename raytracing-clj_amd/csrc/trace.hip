@@ -691,18 +691,17 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // inner children: both -> the near one next, the far one pushed; one
         // -> that one; none -> pop.  The far child is written above the stack
         // top every step (a dead entry unless both were hit): no branch
-        const bool i0 = hit0 && c0 >= 0, i1 = hit1 && c1 >= 0;
+        const bool i0 = hit0 && !l0, i1 = hit1 && !l1;   // (lane masks, no compares)
         const bool sw = tn1 < tn0;
-        const int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
+        int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
         *top = static_cast<StackT>(sw ? c0 : c1);
         top += (i0 && i1) ? 256 : 0;
         if (!(i0 || i1)) {
           if (top == stk0) break;
           top -= 256;
-          node = *top;
-        } else {
-          node = nxt;
+          nxt = *top;
         }
+        node = nxt;
       }
       }
     } else if constexpr (SCAN == SCAN_PK4) {
