@@ -668,7 +668,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // push / pop instead of index arithmetic
       StackT* const stk0 = s_stack + threadIdx.x;
       StackT* top = stk0;
-      for (;;) {
+      bool go = true;
+      while (go) {
         if constexpr (STATS) {
           ++st_sph;
           const uint64_t ex = __builtin_amdgcn_read_exec();
@@ -696,9 +697,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
         *top = static_cast<StackT>(sw ? c0 : c1);
         top += (i0 && i1) ? 256 : 0;
-        if (!(i0 || i1)) {
-          if (top == stk0) break;
-          top -= 256;
+        if (!(i0 || i1)) {   // pop, or (empty stack) leave with a harmless read of entry 0
+          go = top != stk0;
+          top -= go ? 256 : 0;
           nxt = *top;
         }
         node = nxt;
