@@ -458,7 +458,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const float sq = (s == last) ? fabsf(h) : sqrt_rn(disc);
         const float tn = h - sq;
         const float t = tn > tmin ? tn : h + sq;
-        const bool acc = (t > tmin) & ((t < best_t) | ((t == best_t) & (s < best)));
+        // (t, index) < (best_t, best) lexicographically as one 64-bit compare:
+        // t > tmin > 0, so its bits order like the floats; best = -1 is the
+        // largest u32 (and best_t = +inf the largest t) before any hit
+        const uint64_t key = (static_cast<uint64_t>(__float_as_uint(t)) << 32) | static_cast<uint32_t>(s);
+        const uint64_t bkey = (static_cast<uint64_t>(__float_as_uint(best_t)) << 32) | static_cast<uint32_t>(best);
+        const bool acc = (t > tmin) & (key < bkey);
         best_t = acc ? t : best_t;
         best = acc ? s : best;
       };
