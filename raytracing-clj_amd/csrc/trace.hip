@@ -523,10 +523,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         float hh[2 * NP], dd[2 * NP];
         int ii[2 * NP];
         unsigned m = 0;   // candidate bodies of the half
+        // the leaf's pairs from one base address (immediate offsets for the
+        // rest; indexing p + 1 let the compiler rebuild it as -c, a 2nd base)
+        const Pair* const lp = pairs + p;
+        const PidxT* const li = pidx + p;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-          const Pair g = pairs[p + hb + q];
-          const PidxT id = pidx[p + hb + q];
+          const Pair g = lp[hb + q];
+          const PidxT id = li[hb + q];
           const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
           const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
           const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
