@@ -599,8 +599,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
         const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
         const float tf1 = fminf(fminf(tfx.y, tfy.y), tfz.y);
-        hit0 = fmaxf(tn0, tmin) <= fminf(tf0, best_t);
-        hit1 = fmaxf(tn1, tmin) <= fminf(tf1, best_t);
+        // max(tn, t-min) as a bare v_max_f32: fmaxf re-canonicalises t-min
+        // (defined outside the loop) on every step, and the compiler folds
+        // med3(tn, t-min, +inf) back into that fmaxf. t-min is a product
+        // (canonical), and a NaN tn gives t-min either way (conservative).
+        float ntn0, ntn1;
+        asm("v_max_f32 %0, %1, %2" : "=v"(ntn0) : "v"(tn0), "v"(tmin));
+        asm("v_max_f32 %0, %1, %2" : "=v"(ntn1) : "v"(tn1), "v"(tmin));
+        hit0 = ntn0 <= fminf(tf0, best_t);
+        hit1 = ntn1 <= fminf(tf1, best_t);
         c0 = ch.x;
         c1 = ch.y;
       };
