@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         for (int hb = 0; hb < NPL; hb += NP) {
         float hh[2 * NP], dd[2 * NP];
         int ii[2 * NP];
-        unsigned m = 0;   // candidate bodies of the half
+        unsigned nc[2 * NP];   // bit 31: body is a candidate
         // the leaf's pairs from one base address (immediate offsets for the
         // rest; indexing p + 1 let the compiler rebuild it as -c, a 2nd base)
         const Pair* const lp = pairs + p;
@@ -548,13 +548,23 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           // (halves copied to scalars first: __builtin_bit_cast of an
           // ext_vector element read the .x half for .y here)
           const float d0 = disc.x, d1 = disc.y, h0 = h.x, h1 = h.y, k0 = c.x, k1 = c.y;
-          // one v_bitop3_b32 each: LUT 0xf4 = s0 | (s1 & ~s2)
-          const unsigned nx = __builtin_amdgcn_bitop3_b32(__float_as_uint(d0), __float_as_uint(h0),
-                                                          __float_as_uint(k0), 0xf4);
-          const unsigned ny = __builtin_amdgcn_bitop3_b32(__float_as_uint(d1), __float_as_uint(h1),
-                                                          __float_as_uint(k1), 0xf4);
-          m |= ((~nx) >> 31) << (2 * q);
-          m |= ((~ny) >> 31) << (2 * q + 1);
+          // one v_bitop3_b32 each: LUT 0x0b = ~(s0 | (s1 & ~s2))
+          nc[2 * q] = __builtin_amdgcn_bitop3_b32(__float_as_uint(d0), __float_as_uint(h0),
+                                                  __float_as_uint(k0), 0x0b);
+          nc[2 * q + 1] = __builtin_amdgcn_bitop3_b32(__float_as_uint(d1), __float_as_uint(h1),
+                                                      __float_as_uint(k1), 0x0b);
+        }
+        // candidate mask: body j at bit 8j. v_perm_b32's sign selectors (9:
+        // the low source's bit 31, 11: the high source's; 12: zero) gather
+        // two bodies' sign bits as 0x00 / 0xff bytes per instruction, and one
+        // v_bitop3 merges the halves and keeps bit 0 of each byte
+        unsigned m;
+        if constexpr (NP == 2) {
+          const unsigned b01 = __builtin_amdgcn_perm(nc[1], nc[0], 0x0c0c0b09u);
+          const unsigned b23 = __builtin_amdgcn_perm(nc[3], nc[2], 0x0b090c0cu);
+          m = __builtin_amdgcn_bitop3_b32(b01, b23, 0x01010101u, 0xa8);   // (s0 | s1) & s2
+        } else {
+          m = __builtin_amdgcn_perm(nc[1], nc[0], 0x0c0c0b09u) & 0x0101u;
         }
         // one pass of the exact test per candidate: the wave runs it as often
         // as its lane with the most candidates needs (not once per body)
@@ -569,9 +579,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           int s = ii[0];
 #pragma unroll
           for (int j = 1; j < 2 * NP; ++j) {
-            h = k == static_cast<unsigned>(j) ? hh[j] : h;
-            d = k == static_cast<unsigned>(j) ? dd[j] : d;
-            s = k == static_cast<unsigned>(j) ? ii[j] : s;
+            h = k == static_cast<unsigned>(8 * j) ? hh[j] : h;
+            d = k == static_cast<unsigned>(8 * j) ? dd[j] : d;
+            s = k == static_cast<unsigned>(8 * j) ? ii[j] : s;
           }
           consider_tie(h, d, s);
         }
