@@ -48,7 +48,7 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 # node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
 # exact body test (sqrt, root choice) = 4
 FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT = 24, 32, 4
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16j"
+PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16k"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
