@@ -1,29 +1,36 @@
 #!/usr/bin/env python3
-"""bench.py — Mray-samples/s of the MI355X trace kernel on BASELINE.json's C1.
+"""bench.py — Mray-samples/s of the MI355X trace kernel on BASELINE.json's configs.
 
-Workload (BASELINE.json configs[1], the metric's own config): the RTIOW cover
-scene (grid 11 -> 484 bodies, generator seed 42) at 1200x675, 100 spp,
-depth 50, fp32, render seed 1.  A "step" renders one full frame's share:
+Workload (default: C1, BASELINE.json configs[1], the metric's own config):
+the RTIOW cover scene (grid 11 -> 484 bodies, generator seed 42) at
+1200x675, 100 spp, depth 50, fp32, render seed 1.  --workload c2 / c3 / c4
+runs the other configs (C4: cover grid 16 truncated to 1000 bodies, depth 64).
+A "step" renders one frame:
 
-  * --scaling weak (default): every rank renders the whole 1200x675 frame
-    with its own 100-sample stripe (samples [100*rank, 100*rank+100)), so
-    per-GPU work is fixed; ranks share nothing (no collective on the data
-    path; the RNG is keyed by (seed, pixel, sample)).
-  * --scaling strong: the single 100-spp frame is split into interleaved
-    8-row tiles, tile t on rank t % N (the north_star row-tile shard).
+  * --scaling strong (default): the frame is split into interleaved 8-row
+    tiles, tile t on rank t % N -- the north_star row-tile shard of the
+    reference's row-chunk executor (raytracing.clj:157-171), one rank per
+    GPU, no collective on the data path (the RNG is keyed by (seed, pixel,
+    sample), so each rank computes exactly its rows of the 1-GPU frame).
+  * --scaling weak: every rank renders the whole frame with its own sample
+    stripe [spp*rank, spp*(rank+1)), so per-GPU work is fixed.
 
-Inputs (scene table, camera) are resident in HBM before timing; the frame
-stays on the device (host gather is not in `value`).  Timing: W untimed
+Inputs (scene tables, BVH, camera) are resident in HBM before timing; the
+frame stays on the device (host gather is not in `value`).  Timing: W untimed
 warm-up steps, then K steps bracketed by barrier + synchronize, max over
-ranks; kernel duration from HIP events on the launch stream.
+ranks; kernel durations from HIP events on the launch stream.  After the
+timed region rank 0 also times the product's own entry point, rt_render
+(scene cache, N-device fan-out over per-device host threads, D2H into pinned
+memory and the host gather) as `end_to_end`.
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
-      torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+Run:  python bench.py [--gpus N --steps K --warmup W] [--workload c1|c2|c3|c4]
+      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (N > 1)
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import csv
 import ctypes as C
 import json
 import os
@@ -35,29 +42,27 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "raytracing-clj_amd"))
 
-import torch  # noqa: E402  (first: librtclj.so then binds to torch's HIP runtime)
+import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import rtclj  # noqa: E402
+from rtclj import raytracing as R  # noqa: E402
 from rtclj import scenes  # noqa: E402
-from rtclj._lib import check, lib, rt_params  # noqa: E402
+from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0, check, diag_lib, lib, rt_params  # noqa: E402
 from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
 METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
-# executed fp32 flops (fma = 2) of the BVH traversal, per event:
-# node = 2 children x 6 slab planes x (sub + mul); leaf pair = 2 bodies x 16;
-# exact body test (sqrt, root choice) = 4
-FLOPS_NODE, FLOPS_LEAF_PAIR, FLOPS_EXACT = 24, 32, 4
-PMC_DEFAULT = ROOT / "profiles" / "r01" / "pmc_v16k"
-PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (= fp32 MFMA) rate
-PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+PMC_DIR = ROOT / "profiles" / "r02" / "pmc_c1"
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
-FLOPS_PER_SEGMENT = 100    # per-segment hit/scatter/sky work (nominal)
+FLOPS_PER_SEGMENT_NOMINAL = 100   # SURVEY.md §8d's nominal per-segment term
 
 WORKLOADS = {
-    "c1": dict(width=1200, spp=100, depth=50, grid=11, name="C1 RTIOW cover 1200x675 100spp depth50"),
-    "c2": dict(width=3840, spp=500, depth=50, grid=11, name="C2 cover 3840x2160 500spp depth50"),
-    "c4": dict(width=7680, spp=2000, depth=64, grid=16, name="C4 cover(1025) 7680x4320 2000spp depth64"),
+    "c1": dict(width=1200, spp=100, depth=50, scene="cover11", name="C1 RTIOW cover 1200x675 100spp depth50"),
+    "c2": dict(width=3840, spp=500, depth=50, scene="cover11", name="C2 cover(484) 3840x2160 500spp depth50"),
+    "c3": dict(width=3840, spp=1000, depth=50, scene="cover11", name="C3 cover(484) 3840x2160 1000spp depth50"),
+    "c4": dict(width=7680, spp=2000, depth=64, scene="c4", name="C4 cover(1000) 7680x4320 2000spp depth64"),
 }
 
 
@@ -66,98 +71,162 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp (not a bench line)")
-    ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant)")
-    ap.add_argument("--lpp", type=int, default=0, help="lanes per pixel (rt_set_lanes_per_pixel; 0 auto)")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant; 0 = default)")
     ap.add_argument("--schedule", type=int, default=0,
                     help="tile schedule (rt_set_schedule): 0 adaptive longest-first, 1 plain dispatch order")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
+    ap.add_argument("--e2e", choices=["auto", "off"], default="auto", help="time rt_render end to end on rank 0")
+    ap.add_argument("--stats", choices=["auto", "off"], default="auto", help="one untimed stats-build launch")
     return ap.parse_args()
 
 
-def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads):
-    """The oracle's fp64 reference-semantics mode (the C++ restatement of the
-    Clojure path) on a bounded row sample of the same frame, on host cores."""
-    sys.path.insert(0, str(ROOT))
-    import numpy as np
-    import oracle
-    nthreads = max(1, min(threads, os.cpu_count() or 1))
-    t0 = time.perf_counter()
-    _, _, segs, samples = oracle.render(oracle.MODE_REF64, scene.sphere.astype(np.float64), scene.kind,
-                                        scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
-                                        seed=seed, row_step=row_step, nthreads=nthreads)
-    dt = time.perf_counter() - t0
-    rows = (h + row_step - 1) // row_step
-    cpu = "unknown"
+def host_cpus():
+    """CPUs this process can actually use: its affinity set, capped by the
+    cgroup CPU quota (the GPU box's share: its affinity lists every CPU of
+    the machine, its quota 16; 256 threads on a 16-CPU quota run 2.5x
+    slower than 16 -- measured).  Without a readable quota, OMP_NUM_THREADS
+    (which the box sets to its share) caps it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is None and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        quota = float(os.environ["OMP_NUM_THREADS"])   # the box exports its CPU share here
+    n = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return n, aff, quota
+
+
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return "unknown"
+
+
+def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads, gpu_rows, gpu_rows_segs):
+    """The oracle's fp64 reference-semantics mode (the C++ restatement of the
+    Clojure path) on a bounded row sample of the same frame, on host cores;
+    and the parity of the GPU frame's same rows against it (oracle.pin)."""
+    sys.path.insert(0, str(ROOT))
+    import numpy as np
+    import oracle
+    from oracle.pin import BOUNDS, compare, within
+    usable, affinity, quota = host_cpus()
+    nthreads = threads if threads > 0 else usable
+    args = (scene.sphere.astype(np.float64), scene.kind, scene.mat.astype(np.float64), cam.as_list(), cam.defocus,
+            w, h, spp, depth)
+    t0 = time.perf_counter()
+    ref, _, segs, samples = oracle.render(oracle.MODE_REF64, *args, seed=seed, row_step=row_step, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    rows = ref.shape[0]
     # the reference's own setting: a pool of 2 threads (raytracing.clj:157),
     # on a 16x sparser row sample (about the same CPU time)
     step2 = row_step * 16
     t1 = time.perf_counter()
-    _, _, _, samples2 = oracle.render(oracle.MODE_REF64, scene.sphere.astype(np.float64), scene.kind,
-                                      scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
-                                      seed=seed, row_step=step2, nthreads=min(2, nthreads))
+    _, _, _, samples2 = oracle.render(oracle.MODE_REF64, *args, seed=seed, row_step=step2, nthreads=min(2, nthreads))
     dt2 = time.perf_counter() - t1
-    return {"value": samples / dt / 1e6, "unit": "Mray-samples/s", "cores": nthreads, "kind": "port",
-            "sample": f"rows 0,{row_step},{2 * row_step},... ({rows} rows x {w} px x {spp} spp = {samples} samples) "
-                      f"of the same frame, fp64 reference semantics (oracle MODE_REF64), {dt:.1f} s",
-            "seconds": dt, "segments_per_sample": segs / max(samples, 1), "cpu_model": cpu,
-            "host": platform.node(),
-            "two_threads": {"value": samples2 / dt2 / 1e6, "cores": min(2, nthreads),
-                            "sample": f"every {step2}th row ({samples2} samples), {dt2:.1f} s: the reference's "
-                                      f"pool-size 2 (raytracing.clj:157)"}}
+    res = {"value": samples / dt / 1e6, "unit": "Mray-samples/s", "cores": nthreads, "kind": "port",
+           "sample": f"rows 0,{row_step},{2 * row_step},... ({rows} rows x {w} px x {spp} spp = {samples} samples) "
+                     f"of the same frame, fp64 reference semantics (oracle MODE_REF64), {dt:.1f} s on "
+                     f"{nthreads} threads",
+           "seconds": dt, "segments_per_sample": segs / max(samples, 1), "cpu_model": cpu_model(),
+           "host": platform.node(), "affinity_cpus": affinity, "cgroup_quota_cpus": quota,
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "two_threads": {"value": samples2 / dt2 / 1e6, "cores": min(2, nthreads),
+                           "sample": f"every {step2}th row ({samples2} samples), {dt2:.1f} s: the reference's "
+                                     f"pool-size 2 (raytracing.clj:157)"}}
+    parity = None
+    if gpu_rows is not None:
+        st = compare(ref, segs / samples, gpu_rows, gpu_rows_segs / samples, by=max(1, min(9, rows // 8)))
+        ok = within(st)
+        parity = {"against": "oracle MODE_REF64 (the Clojure path in double), same rows, same seed",
+                  "rows": f"0,{row_step},...", "stats": st, "bounds": BOUNDS, "pass": all(ok.values()),
+                  "checks": ok}
+    return res, parity
 
 
-# traversal variant -> (its stats build, body pairs per leaf)
-BVH_STATS = {0: (17, 2), 16: (17, 2), 17: (17, 2), 18: (19, 4), 19: (19, 4), 11: (13, 1), 13: (13, 1), 14: (15, 1), 15: (15, 1)}
+# the statistics build of each product traversal (the diagnostic library), and
+# body pairs per leaf of its tree
+STATS_OF = {16: (17, 2), 18: (19, 4), 12: (13, 1), 5: (7, 0)}
 
 
-def bvh_counters(ds, cam, p, out, counters, sh, variant):
-    """One untimed launch of the stats build of the same frame and traversal
-    (variant 17 for the default 16, 13 for 11): per-segment node visits,
-    leaf pair tests, exact tests (rt_debug_stats)."""
-    sv, pairs_per_leaf = BVH_STATS[lib.rt_resolve_variant(ds)]
-    old = lib.rt_set_variant(sv)
+def stats_leg(scene, cam, p, device, out_numel):
+    """One untimed launch of the statistics build of the same frame, scene and
+    traversal in the diagnostic library: counted executed flops per segment
+    (fma = 2), BVH node / leaf / exact-test counts, wave-level events."""
+    d = diag_lib()
+    ds = C.c_void_p()
+    check(d.rt_scene_upload(device, C.byref(scene.c), C.byref(ds)))
     try:
-        dbg = (C.c_uint64 * 16)()
-        check(lib.rt_debug_stats(dbg))                  # clear
-        counters.zero_()
-        check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()),
-                            C.c_void_p(counters.data_ptr()), sh))
-        torch.cuda.synchronize()
-        check(lib.rt_debug_stats(dbg))
-        segs = float(counters[0].item())
+        v = lib_resolved_variant(scene, device)
+        sv, pairs_per_leaf = STATS_OF.get(v, (None, None))
+        if sv is None:
+            return None
+        old = d.rt_set_variant(sv)
+        out = torch.empty(out_numel, dtype=torch.float32, device=torch.device("cuda", device))
+        cnt = torch.zeros(2, dtype=torch.int64, device=out.device)
+        dbg = (C.c_uint64 * 32)()
+        try:
+            check(d.rt_debug_stats(dbg))   # clear
+            s = torch.cuda.current_stream(out.device)
+            check(d.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), C.c_void_p(cnt.data_ptr()),
+                              C.c_void_p(s.cuda_stream)))
+            torch.cuda.synchronize()
+            check(d.rt_debug_stats(dbg))
+        finally:
+            d.rt_set_variant(old)
+        segs, smp = (float(x) for x in cnt.cpu().tolist())
     finally:
-        lib.rt_set_variant(old)
+        d.rt_scene_free(ds)
     wi = max(dbg[0], 1)
-    return {"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs, "exact_tests": dbg[4] / segs,
-            "stats_variant": sv,
-            # wave-level events per wave loop iteration (what the VALU issues for)
-            "per_wave_iter": {"wave_iters_per_sample": wi / max(float(counters[1].item()), 1.0),
-                              "lanes_active": dbg[1] / wi / 64.0, "trav_steps": dbg[6] / wi,
-                              "trav_lane_eff": dbg[7] / max(dbg[6], 1) / 64.0,
-                              "leaf_passes": dbg[12] / wi, "exact_passes": dbg[13] / wi,
-                              "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi}}
+    res = {"stats_variant": sv, "flops_per_segment": dbg[18] / segs, "segments_per_sample": segs / smp,
+           "per_wave_iter": {"wave_iters_per_sample": wi / smp, "lanes_active": dbg[1] / wi / 64.0,
+                             "fresh_blocks": dbg[16] / wi, "fresh_lanes": dbg[17] / max(dbg[16], 1),
+                             "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi}}
+    if v != 5:
+        res.update({"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs,
+                    "exact_tests": dbg[4] / segs})
+        res["per_wave_iter"].update({"trav_steps": dbg[6] / wi, "trav_lane_eff": dbg[7] / max(dbg[6], 1) / 64.0,
+                                     "leaf_passes": dbg[12] / wi, "exact_passes": dbg[13] / wi})
+    return res
+
+
+_resolved = {}
+
+
+def lib_resolved_variant(scene, device):
+    return _resolved[(id(scene), device)]
 
 
 def _pmc_avg(passes, counters):
-    """Per-dispatch averages of PMC counters over the timed kernel's launches
-    (trace_kernel, not its stats build) in the committed rocprofv3 passes."""
-    import csv
+    """Per-dispatch averages of PMC counters over the product kernel's
+    launches (trace_kernel, not the stats build) in the committed rocprofv3
+    passes (profiles/pmc.sh; one counter group per pass)."""
     acc = {}
     for name in passes:
-        f = PMC_DEFAULT / f"{name}.csv"
+        f = PMC_DIR / f"{name}.csv"
         if not f.exists():
             return None
         for r in csv.DictReader(open(f)):
@@ -169,51 +238,69 @@ def _pmc_avg(passes, counters):
 
 
 def pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (separate
-    FETCH_SIZE / WRITE_SIZE runs, KB units; gfx950 FETCH_SIZE counts half the
-    bytes of wide streaming reads -> x2, MI355X_MICROARCH.md §HBM)."""
+    """HBM bytes per launch (FETCH_SIZE and WRITE_SIZE in their own passes, KB
+    units; gfx950's FETCH_SIZE counts half the bytes of wide streaming reads ->
+    x2, MI355X_MICROARCH.md §HBM)."""
     v = _pmc_avg(("fetch", "write"), ("FETCH_SIZE", "WRITE_SIZE"))
     if v is None:
-        return None, None
-    return (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, str(PMC_DEFAULT.relative_to(ROOT))
-
-
-def occupancy(ds, p, with_pmc, n_simd=1024, n_xcd=8):
-    """Resident waves per SIMD: the launch's limit (HIP occupancy query with its
-    dynamic LDS; VGPRs) and the measured mean over the timed kernel's launches
-    from the committed PMC pass (SQ_WAVE_CYCLES in 4-cycle units summed over
-    the SIMDs, vs GRBM_GUI_ACTIVE summed over the XCDs)."""
-    o = (C.c_int * 4)()
-    check(lib.rt_launch_occupancy(ds, C.byref(p), o))
-    limit = min(8.0, o[0] * 4 / 4.0)   # 256-thread workgroups per CU x 4 waves / 4 SIMDs
-    res = {"limit_waves_per_simd": limit, "workgroups_per_cu": o[0], "vgprs": o[1], "lds_bytes_per_wg": o[2],
-           "lanes_per_pixel_shape": o[3], "hw_max_waves_per_simd": 8}
-    v = _pmc_avg(("waves",), ("SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE")) if with_pmc else None
-    if v is not None:
-        mean = v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
-        res.update({"mean_waves_per_simd": mean, "frac_of_limit": mean / limit, "frac_of_hw_max": mean / 8.0,
-                    "source": str(PMC_DEFAULT.relative_to(ROOT))})
-    return res
+        return None
+    return {"bytes": (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, "fetch_bytes_x2": 2048.0 * v["FETCH_SIZE"],
+            "write_bytes": 1024.0 * v["WRITE_SIZE"], "source": str(PMC_DIR.relative_to(ROOT))}
 
 
 def pmc_valu(n_simd=1024, n_xcd=8):
-    """VALU issue picture of the same launches: the fraction of cycles each
-    SIMD issues a VALU instruction (SQ_ACTIVE_INST_VALU, 4-cycle units,
-    summed over the SIMDs, vs GRBM_GUI_ACTIVE summed over the XCDs) and the
-    mean fraction of the 64 lanes active per VALU instruction."""
+    """VALU issue picture of the same launches: issue_busy = fraction of
+    4-cycle slots in which a SIMD issues a VALU instruction
+    (SQ_ACTIVE_INST_VALU x 4 / SIMDs vs GRBM_GUI_ACTIVE / XCDs); lanes_active
+    = mean fraction of the 64 lanes active per VALU instruction."""
     v = _pmc_avg(("insts", "waves"), ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU",
-                                      "GRBM_GUI_ACTIVE"))
+                                      "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES"))
     if v is None:
         return None
     busy = v["SQ_ACTIVE_INST_VALU"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
     lanes = v["SQ_THREAD_CYCLES_VALU"] / v["SQ_INSTS_VALU"] / 64.0
-    return {"issue_busy": busy, "lanes_active": lanes, "valu_insts": v["SQ_INSTS_VALU"],
-            "source": str(PMC_DEFAULT.relative_to(ROOT)),
-            "note": "the binding limit: VALU issue slots (a wave64 instruction takes 4 cycles whatever its "
-                    "active lanes); issue_busy ~1 = every SIMD issues a VALU instruction every 4 cycles "
-                    "(SQ_ACTIVE_INST_VALU counts per wave, so overlapping multi-cycle instructions can read "
-                    "a little above 1); executed-flop frac = issue_busy x lanes_active x (flops per issued "
-                    "lane-instruction)"}
+    return {"issue_busy": busy, "lanes_active": lanes, "issue_utilisation": busy * lanes,
+            "valu_insts": v["SQ_INSTS_VALU"],
+            "mean_waves_per_simd": v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd),
+            "source": str(PMC_DIR.relative_to(ROOT))}
+
+
+def occupancy(ds, p):
+    o = (C.c_int * 4)()
+    check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+    return {"limit_waves_per_simd": min(8.0, o[0] * 4 / 4.0), "workgroups_per_cu": o[0], "vgprs": o[1],
+            "lds_bytes_per_wg": o[2], "variant": o[3], "hw_max_waves_per_simd": 8}
+
+
+def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=3):
+    """rt_render, the product entry point the JNI shim calls: the scene cache
+    (the first call uploads and builds the BVHs), the N-device fan-out with
+    one host thread per device, D2H into pinned memory and the host gather
+    into one caller buffer.  Warm call first, then `reps` timed calls."""
+    import numpy as np
+    visible = lib.rt_device_count()
+    flags = RT_FLAG_SHARDS_ON_DEVICE0 if n_dev > visible else 0
+    out = np.empty((H, W, 3), np.float32)
+    first = {}
+    t0 = time.perf_counter()
+    R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=first)
+    first_wall = (time.perf_counter() - t0) * 1e3
+    runs = []
+    for _ in range(reps):
+        st = {}
+        t0 = time.perf_counter()
+        out = R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=st)
+        st["wall_ms"] = (time.perf_counter() - t0) * 1e3
+        runs.append(st)
+    best = min(runs, key=lambda r: r["total_ms"])
+    return {"entry": "rt_render (include/rt.h)", "n_devices": best["n_devices"],
+            "shards_on_device0": bool(flags), "total_ms": best["total_ms"], "kernel_ms_max": best["kernel_ms"],
+            "kernel_ms_mean": best["kernel_ms_mean"], "imbalance": best["kernel_ms"] / best["kernel_ms_mean"],
+            "upload_ms": best["upload_ms"], "gather_ms": best["gather_ms"], "scene_cached": best["scene_cached"],
+            "value": W * H * spp / (best["total_ms"] * 1e-3) / 1e6, "unit": "Mray-samples/s",
+            "first_call": {"total_ms": first["total_ms"], "upload_ms": first["upload_ms"],
+                           "scene_cached": first["scene_cached"], "python_wall_ms": first_wall},
+            "repeats": reps}, out
 
 
 def main():
@@ -234,8 +321,8 @@ def main():
     dev = torch.device("cuda", device)
     # The render exchanges nothing between ranks (pixels/samples are
     # independent; RNG keyed by (seed, pixel, sample)): the only cross-rank
-    # traffic is the barrier and the max/sum of three timing scalars, done on
-    # the host over gloo (BENCH_DIST_BACKEND=nccl moves them to RCCL).
+    # traffic is the barrier and the timing scalars, on the host over gloo
+    # (BENCH_DIST_BACKEND=nccl moves them to RCCL).
     backend = os.environ.get("BENCH_DIST_BACKEND", "gloo")
     if world > 1:
         # C-level banners (gloo prints "connected to N peer ranks") go to
@@ -250,22 +337,21 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
-    red_dev = dev if backend == "nccl" else torch.device("cpu")
-    lib.rt_set_variant(a.variant)
-    lib.rt_set_lanes_per_pixel(a.lpp)
-    lib.rt_set_schedule(a.schedule)
+    check(lib.rt_set_variant(a.variant))
+    check(lib.rt_set_schedule(a.schedule))
 
     wl = dict(WORKLOADS[a.workload])
     if a.spp:
         wl["spp"] = a.spp
     W = wl["width"]
-    H = rtclj.raytracing.image_height(W)
+    H = R.image_height(W)
     spp, depth = wl["spp"], wl["depth"]
-    scene = scenes.cover(wl["grid"], 42)
+    scene = scenes.cover_c4() if wl["scene"] == "c4" else scenes.cover(11, 42)
     cam = scenes.cover_camera(W, H)
 
     ds = C.c_void_p()
     check(lib.rt_scene_upload(device, C.byref(scene.c), C.byref(ds)))
+    _resolved[(id(scene), device)] = lib.rt_resolve_variant(ds)
     p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
     rows = check(lib.rt_rows_out(C.byref(p)))
     assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
@@ -300,78 +386,111 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     cnt = counters.to("cpu").tolist()
-    local_stats = torch.tensor([elapsed, max(kern_ms), sum(kern_ms) / len(kern_ms)], dtype=torch.float64)
-    tot = torch.tensor([float(cnt[0]), float(cnt[1])], dtype=torch.float64)
+    mine = {"rank": rank, "device": device, "elapsed_s": elapsed, "kernel_ms_avg": sum(kern_ms) / len(kern_ms),
+            "kernel_ms_max": max(kern_ms), "rows": rows, "segments": cnt[0], "samples": cnt[1]}
+    per_rank = [mine]
     if world > 1:
-        ls, tt = local_stats.to(red_dev), tot.to(red_dev)
-        dist.all_reduce(ls, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
-        local_stats, tot = ls.cpu(), tt.cpu()
-    elapsed, kern_max_ms, kern_avg_ms = local_stats.tolist()
-    segs_total, samples_total = tot.tolist()
-    bvh = (bvh_counters(ds, cam, p, out, counters, sh, a.variant)
-           if rank == 0 and lib.rt_resolve_variant(ds) in BVH_STATS else None)
-    # the committed PMC passes were taken on C1's default launch: only that
-    # workload's line quotes them
-    pmc_ok = a.workload == "c1" and not a.spp and a.variant == 0 and a.lpp == 0 and a.scaling == "weak"
-    occ = occupancy(ds, p, pmc_ok) if rank == 0 else None
-    lib.rt_scene_free(ds)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    elapsed = max(r["elapsed_s"] for r in per_rank)
+    segs_total = sum(r["segments"] for r in per_rank)
+    samples_total = sum(r["samples"] for r in per_rank)
+    kern_avg_ms = mine["kernel_ms_avg"]
 
+    res = None
     if rank == 0:
-        samples_per_step = samples_total / a.steps
-        value = samples_per_step * a.steps / elapsed / 1e6
+        occ = occupancy(ds, p)
+        stats = stats_leg(scene, cam, p, device, rows * W * 3) if a.stats == "auto" else None
+        value = samples_total / elapsed / 1e6
         seg_per_sample = segs_total / max(samples_total, 1)
-        # dominant kernel, per launch on this rank (rank-0 share at N>1)
+        # the dominant (only) kernel, per launch on rank 0
         launch_samples = rows * W * spp
         launch_segs = seg_per_sample * launch_samples
-        bf_flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT)
+        kms = [r["kernel_ms_avg"] for r in per_rank]
+        pmc_ok = a.workload == "c1" and not a.spp and a.variant == 0 and world == 1
+        traffic = pmc_traffic() if pmc_ok else None
+        valu = pmc_valu() if pmc_ok else None
+        bf_flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT_NOMINAL)
         bf_tflops = bf_flops / (kern_avg_ms * 1e-3) / 1e12
-        if bvh is not None:
-            per_seg = (FLOPS_NODE * bvh["nodes"] + FLOPS_LEAF_PAIR * bvh["leaf_pairs"] +
-                       FLOPS_EXACT * bvh["exact_tests"] + FLOPS_PER_SEGMENT)
-            work = (f"BVH traversal, executed fp32 work per segment = 24 x {bvh['nodes']:.2f} nodes + "
-                    f"32 x {bvh['leaf_pairs']:.2f} leaf pairs (the big bodies' leaf included) + "
-                    f"4 x {bvh['exact_tests']:.2f} exact tests + 100 = {per_seg:.0f} flops "
-                    f"(counters: one untimed stats launch)")
-        else:
-            per_seg = FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT
-            work = f"linear scan, executed fp32 work per segment = 17 x {len(scene)} bodies + 100"
-        tflops = launch_segs * per_seg / (kern_avg_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
+                "traffic": traffic["bytes"] if traffic else None}
+        if stats is not None:
+            fl = stats["flops_per_segment"]
+            tflops = launch_segs * fl / (kern_avg_ms * 1e-3) / 1e12
+            roof.update(achieved=tflops, frac=tflops / PEAK_FP32_TFLOPS, flops_per_segment=fl,
+                        flops_source=f"counted: executed fp32 flops per lane (fma = 2), one untimed launch of the "
+                                     f"statistics build (variant {stats['stats_variant']}, lib/librtclj_diag.so) of "
+                                     f"the same frame")
+        if valu is not None:
+            roof.update(issue_busy=valu["issue_busy"], lanes_active=valu["lanes_active"],
+                        issue_utilisation=valu["issue_utilisation"])
+        roof["note"] = ("VALU-issue bound: branchy per-ray fp32 work, no GEMM shape (MFMA unused), HBM not binding "
+                        "(hbm_roofline). peak = the packed fp32 vector rate. issue_utilisation = issue_busy x "
+                        "lanes_active (PMC): the SIMDs issue a VALU instruction in nearly every slot, and "
+                        "lanes_active of the 64 lanes do work in it.")
+        roof["brute_force_equivalent"] = {
+            "tflops": bf_tflops, "frac": bf_tflops / PEAK_FP32_TFLOPS,
+            "note": f"SURVEY.md §8d's formula (17 x {len(scene)} bodies + 100 per segment) prices the linear scan; "
+                    f"the BVH tests ~1/19 of those bodies and returns the scan's hits bit for bit "
+                    f"(tests/test_gpu_parity.py::test_bvh_bit_exact_on_full_c1_and_reference), so at "
+                    f"{bf_tflops / PEAK_FP32_TFLOPS:.2f}x of peak that formula does not apply to this kernel"}
         hbm_bytes = rows * W * 12 + len(scene) * 32
         gbs = hbm_bytes / (kern_avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic() if pmc_ok else (None, "no committed PMC pass for this workload")
         res = {
             "metric": METRIC, "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": a.scaling, "vs_baseline": None, "dtype": "fp32",
-            "data": f"synthetic: RTIOW cover scene (grid {wl['grid']}, {len(scene)} bodies, generator seed 42), "
-                    f"render seed {a.seed}",
+            "data": f"synthetic: RTIOW cover scene ({len(scene)} bodies, generator seed 42), render seed {a.seed}",
             "config": {"workload": wl["name"] if not a.spp else f"{wl['name']} (spp override {spp})",
-                       "width": W, "height": H, "spp_per_gpu": spp, "max_depth": depth, "bodies": len(scene),
-                       "parallelism": ("sample-stripe x%d (weak)" % world) if a.scaling == "weak"
-                       else ("row-tile 8 x%d (strong)" % world), "variant": a.variant,
+                       "width": W, "height": H, "spp": spp, "max_depth": depth, "bodies": len(scene),
+                       "parallelism": ("row-tile 8 x%d (strong)" % world) if a.scaling == "strong"
+                       else ("sample-stripe x%d (weak)" % world), "variant": a.variant,
                        "tile_schedule": "adaptive longest-first" if a.schedule == 0 else "dispatch order"},
-            "roofline": {"bound": "mfma", "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tflops / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "note": f"compute-bound fp32 on the VALU (branchy per-ray FP work, no GEMM shape: MFMA unused); "
-                                 f"peak = the fp32 dense peak (vector = MFMA for fp32); {work}. "
-                                 f"Brute-force-equivalent (SURVEY §8d: 17 x {len(scene)} + 100 per segment): "
-                                 f"{bf_tflops:.1f} TF/s. traffic = HBM bytes/launch from {traffic_src} "
-                                 f"(FETCH x2 + WRITE)"},
+            "roofline": roof,
             "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
-                             "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB) + bodies*32"},
-            "valu": pmc_valu() if pmc_ok else None,
-            "occupancy": occ,
-            "bvh_per_segment": bvh,
-            "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": kern_max_ms,
-            "segments_per_sample": seg_per_sample, "samples_per_step": samples_per_step,
-            "kernel": "rtclj::trace_kernel<SRC,SCAN,LPP> (variant %d; default = 16: BVH with 4-body leaves in LDS, 8x8-pixel sample pool per workgroup)" % a.variant,
-            "cpu_baseline": None,
+                             "frac": gbs / PEAK_HBM_GBS, "traffic": traffic["bytes"] if traffic else None,
+                             "traffic_detail": traffic,
+                             "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB written once) + "
+                                     "bodies*32 (scene read); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch"},
+            "valu": valu, "occupancy": occ, "stats_build": stats,
+            "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": mine["kernel_ms_max"],
+            "per_rank": {"kernel_ms_avg": kms, "rows": [r["rows"] for r in per_rank],
+                         "imbalance": max(kms) / (sum(kms) / len(kms))},
+            "segments_per_sample": seg_per_sample, "samples_per_step": samples_total / a.steps,
+            "kernel": "rtclj::trace_kernel<SRC,SCAN,STATS> (default: BVH with 4-body leaves in LDS, 8x8-pixel "
+                      "sample pool per 256-thread workgroup, fixed-point colour sums in LDS)",
+            "end_to_end": None, "cpu_baseline": None, "parity": None,
         }
+    if a.e2e == "auto":
+        # the product fan-out over world devices, timed on rank 0 while the
+        # other ranks wait at the barrier
+        barrier()
+        if rank == 0:
+            res["end_to_end"], frame = end_to_end(scene, cam, W, H, spp, depth, a.seed, world)
+        barrier()
+    if rank == 0:
         if a.cpu_baseline == "auto" and world == 1:
-            res["cpu_baseline"] = cpu_baseline(scene, cam, W, H, spp, depth, a.seed, a.cpu_row_step, a.cpu_threads)
+            import numpy as np
+            gpu_rows = segs_rows = None
+            if a.scaling == "strong":
+                # the GPU frame's rows 0, s, 2s, ... and their own segment count
+                # (one untimed launch of just those rows: 1-row tiles, stride s)
+                pr = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
+                               row_tile=1, tile_first=0, tile_step=a.cpu_row_step)
+                nr = check(lib.rt_rows_out(C.byref(pr)))
+                o2 = torch.empty(nr * W * 3, dtype=torch.float32, device=dev)
+                c2 = torch.zeros(2, dtype=torch.int64, device=dev)
+                check(lib.rt_launch(ds, C.byref(cam), C.byref(pr), C.c_void_p(o2.data_ptr()),
+                                    C.c_void_p(c2.data_ptr()), sh))
+                torch.cuda.synchronize()
+                gpu_rows = o2.cpu().numpy().reshape(nr, W, 3)
+                full = out.cpu().numpy().reshape(H, W, 3)
+                assert np.array_equal(gpu_rows, full[::a.cpu_row_step]), "row launch != the timed frame's rows"
+                segs_rows = float(c2[0].item())
+            res["cpu_baseline"], res["parity"] = cpu_baseline(scene, cam, W, H, spp, depth, a.seed, a.cpu_row_step,
+                                                              a.cpu_threads, gpu_rows, segs_rows)
         print(json.dumps(res), flush=True)
+    lib.rt_scene_free(ds)
     if world > 1:
         dist.destroy_process_group()
 

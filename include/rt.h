@@ -31,6 +31,12 @@
 extern "C" {
 #endif
 
+/* The library is built with -fvisibility=hidden: exactly the functions
+ * declared here are exported. */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
   RT_OK = 0,
@@ -49,6 +55,11 @@ enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2, RT_NONE = 3 };
 
 /* Maximum spheres per scene (LDS-resident sphere table, 16 B each). */
 #define RT_MAX_SPHERES 8192
+
+/* Maximum samples per pixel of one call (the pixel's fixed-point colour sums,
+ * 2^-24 units per sample, stay below 2^64; larger counts: several calls with
+ * sample_begin). */
+#define RT_MAX_SPP (1 << 24)
 
 /* ---- scene: the reference's `hittables` vector (raytracing.clj:63-78) -----
  * Bodies are tested in array order; on equal t the earlier body wins, exactly
@@ -111,13 +122,19 @@ typedef struct rt_params {
  * any other (rt_camera_setup with defocus_angle 0). */
 #define RT_FLAG_REALM 2
 
-/* ---- per-call statistics (device-side counters) ------------------------- */
+/* ---- per-call statistics (device-side counters, host timers) ------------ */
 typedef struct rt_stats {
   uint64_t segments;      /* hit-anything calls (raytracing.clj:48)            */
   uint64_t samples;       /* compute-pixel loop iterations (:142-154)          */
   double kernel_ms;       /* max over devices of the trace-kernel time         */
   double total_ms;        /* wall time of the whole call incl. H2D/D2H         */
   int n_devices;          /* devices used                                      */
+  int scene_cached;       /* devices whose scene came from the library's cache */
+  double upload_ms;       /* max over devices: scene lookup / H2D upload + BVH  */
+  double gather_ms;       /* max over devices: D2H into pinned memory + host
+                             scatter of the device's row tiles into out_rgb    */
+  double kernel_ms_mean;  /* mean over devices of the trace-kernel time
+                             (load imbalance = kernel_ms / kernel_ms_mean)     */
 } rt_stats;
 
 /* ========================= host-side helpers =========================== */
@@ -171,9 +188,20 @@ int rt_scene_cover(int grid, uint64_t seed, float* sphere, int* kind, float* mat
  * rows_out x width x 3, the mean over spp (compute-pixel's accum/spp,
  * raytracing.clj:155).  Fans out over p->n_devices GPUs inside the call
  * (one host thread per device, interleaved row tiles, host-side gather; no
- * collectives).  tile_first/tile_step must be 0 here.  stats may be NULL. */
+ * collectives).  tile_first/tile_step must be 0 here.  stats may be NULL.
+ *
+ * The device copy of the scene (tables + BVHs) is cached per device by the
+ * scene's content (a hash, then a byte compare): a repeated call with the
+ * same bodies skips the upload and the BVH builds, and its launches reuse
+ * the per-device stream whose adaptive tile order (rt_set_schedule) the
+ * previous call recorded.  The library keeps copies, never caller pointers.
+ * Output bits never depend on the cache. */
 int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p,
               float* out_rgb, size_t out_len, rt_stats* stats);
+
+/* Drop rt_render's cached device scenes, streams and staging buffers (those
+ * not in use by a concurrent call).  Returns the number of scenes dropped. */
+int rt_cache_clear(void);
 
 /* Device-resident path (inputs already in HBM; used by the benchmark). */
 typedef struct rt_dscene rt_dscene;
@@ -185,20 +213,22 @@ int rt_scene_free(rt_dscene* ds);
 int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
 
-/* Kernel variant selector for A/B measurement (all variants give identical
- * bits): 0 = default (16, or 18 when the 4-body tree's LDS image exceeds
- * 32 KB and the 8-body tree's is smaller); 16 = BVH traversal, 4 bodies per
- * leaf, nodes and leaf bodies in LDS, 17 = 16 with statistics, 18 / 19 = the
- * same with 8 bodies per leaf; 11 = the same with 2 bodies
- * per leaf, 12 = 11 reading the tree from global memory (used when a tree
- * does not fit LDS), 13 = 11 with statistics, 14 / 15 = 11 with a
- * speculative while-while traversal (+ statistics); 1 = sphere table in LDS, one body per step;
- * 2 = table through the scalar cache, one body per step; 4 = LDS table,
- * bodies in groups of 4 with the next group prefetched; 5 = scalar-cache
- * table, grouped; 8 / 9 = 4 / 5 with two bodies per packed-fp32
- * instruction; 3, 6, 7, 10 = 1, 4, 5, 9 with wave-level statistics counters
- * (diagnostic builds; slower).  Returns the previous value; applies to
- * subsequent launches in this process. */
+/* Kernel variant selector (all variants give identical bits).  The product
+ * library holds: 0 = default (16, or 18 when the 4-body tree's LDS image
+ * would cap a CU below 5 workgroups and the 8-body tree's is smaller);
+ * 16 = BVH traversal, 4 bodies per leaf, nodes and leaf bodies in LDS;
+ * 18 = the same with 8 bodies per leaf; 12 = BVH with 2 bodies per leaf read
+ * from global memory (the fallback for a tree too big for LDS); 5 = linear
+ * scan, bodies in groups of 4 through the scalar cache (the fallback for a
+ * tree too deep for the stack).  The diagnostic build lib/librtclj_diag.so
+ * (make diag) adds: 1 / 2 = simple scan, table in LDS / scalar cache;
+ * 4 = grouped scan, table in LDS (north_star's LDS-staged sphere list);
+ * 8 / 9 = packed-fp32 scan, LDS / scalar; 11 = BVH in LDS, 2 bodies per leaf;
+ * 14 = 11 with a speculative while-while traversal; and the statistics builds
+ * 3, 6, 7, 10, 13, 15, 17, 19 (= 1, 4, 5, 9, 11, 14, 16, 18 with wave-level
+ * counters, rt_debug_stats).  Returns the previous value, or RT_E_ARG for a
+ * variant this build does not hold.  Applies to subsequent launches in this
+ * process (an atomic, read once per launch). */
 int rt_set_variant(int variant);
 
 /* The kernel variant rt_launch would run for ds under the current selector
@@ -209,55 +239,49 @@ int rt_resolve_variant(const rt_dscene* ds);
 /* Occupancy of the launch rt_launch would make for (ds, p) under the current
  * selectors (diagnostic): out4 = {256-thread workgroups per CU (HIP occupancy
  * query with the launch's dynamic LDS), VGPRs per lane, LDS bytes per
- * workgroup, lanes-per-pixel shape}. */
+ * workgroup, the variant}. */
 int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int* out4);
 
-/* Launch shape.  1, 2, 4: lanes per pixel, each lane running a fixed share
- * of the pixel's four sample stripes.  -1 / -2: the sample pool, a wave owns
- * 4 x 4 / 8 x 8 pixels and every (pixel, sample) pair of them; a lane whose
- * path ends takes the next pair, the colours go to a scratch and are summed
- * per stripe in sample order after the pool.  -3: one pool of 8 x 8 pixels
- * per workgroup, shared by its 4 waves.  Pools exist for the BVH variants 11,
- * 13, 16-19; the scratch is per scene and stream, about 12 bytes per sample
- * up to 1/8 of the device memory a launch (RTCLJ_POOL_BYTES overrides), more
- * launches beyond.  0 = automatic: -3 where the
- * variant has it, else by frame size.  Changes the launch shape, never the
- * result.  Returns the previous value. */
-int rt_set_lanes_per_pixel(int lpp);
-
 /* Tile dispatch order of rt_launch.  0 (default) = adaptive: every launch
- * records how long each tile's waves ran, and a one-block sort enqueued after
- * it (same stream, no host sync) turns that into a longest-first order; the
- * next launch on the same scene and stream with the same launch shape (width,
- * row selection, lanes per pixel; camera, spp, seed, flags and the kernel
- * variant may differ) dispatches its tiles in that order, so the slow tiles do not
- * trail the kernel's end.  A launch of another shape runs in plain order and
- * re-keys the record (per scene, up to 8 streams; launches on further streams
- * are unscheduled).  1 = always plain order.  Changes timing only: every
- * pixel is computed the same way in any order (bit-identical output).
- * Returns the previous value. */
+ * records how long each 8 x 8 pixel tile's waves ran, and a one-block sort
+ * enqueued after it (same stream, no host sync) turns that into a
+ * longest-first order; the next launch on the same scene and stream with the
+ * same launch shape (width, row selection; camera, spp, seed, flags and the
+ * kernel variant may differ) dispatches its tiles in that order, so the slow
+ * tiles do not trail the kernel's end.  A launch of another shape runs in
+ * plain order and re-keys the record (per scene, up to 8 streams; launches on
+ * further streams are unscheduled).  1 = always plain order.  Changes timing
+ * only: every pixel is computed the same way in any order (bit-identical
+ * output).  Returns the previous value, RT_E_ARG for another mode. */
 int rt_set_schedule(int mode);
 
-/* Diagnostic counters of the stats variants (3, 6, 7, 10, 13, 15, 17) since the last
- * call (then cleared), 16 values: [0] wave loop iterations, [1] active lanes
- * summed over them, [2] body tests per wave (scan) / node visits per lane
- * (BVH), [3] candidate blocks per wave (scan) / leaf tests per lane (BVH),
- * [4] lanes in candidate blocks / exact body tests (BVH), [5] waves,
- * [6] BVH wave-level traversal iterations, [7] lanes active in them,
- * [8..11] shader clocks per wave spent in camera sampling, hit search,
- * shading, accumulation (s_memtime; summed over waves), [12] BVH
+/* Diagnostic counters of the stats variants (diagnostic build) since the
+ * last call (then cleared), summed over devices, 32 values: [0] wave loop
+ * iterations, [1] active lanes summed over them, [2] body tests per wave
+ * (scan) / node visits per lane (BVH), [3] candidate blocks per wave (scan) /
+ * leaf tests per lane (BVH), [4] lanes in candidate blocks / exact body
+ * tests (BVH), [5] waves, [6] BVH wave-level traversal iterations, [7] lanes
+ * active in them, [8..11] shader clocks per wave spent in camera sampling,
+ * hit search, shading, accumulation (s_memtime; summed over waves), [12] BVH
  * wave-level leaf passes, [13] wave-level exact-test passes, [14] / [15]
- * wave-level trips of the random-unit-vec3 / defocus-disk rejection loops.
- * Synchronises the device. */
-int rt_debug_stats(uint64_t* out16);
+ * wave-level trips of the random-unit-vec3 / defocus-disk rejection loops,
+ * [16] / [17] wave-level camera-sample blocks / lanes in them, [18] executed
+ * fp32 flops (per lane, fma = 2), [19..31] 0.
+ * Synchronises the devices. */
+int rt_debug_stats(uint64_t* out32);
 
-/* Diagnostic wave timeline of variant 3's last launches: n_waves x
- * {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID}; returns the count. */
-int rt_debug_waves(uint64_t* out, size_t n_waves);
+/* Diagnostic wave timeline of the stats variants' last launches on `device`:
+ * n_waves x {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID}; returns
+ * the count. */
+int rt_debug_waves(int device, uint64_t* out, size_t n_waves);
 
 int rt_device_count(void);
 const char* rt_last_error(void);
 const char* rt_version(void);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 
 #ifdef __cplusplus
 }

@@ -19,9 +19,10 @@
 //     (raytracing-clj_amd/csrc/trace.hip) restated op for op:
 //     explicit fmaf, correctly rounded / and sqrt, normalisation by one
 //     reciprocal (v * (1/|v|), (p - C) * (1/r)), unit-direction hit test,
-//     stackless throughput, exact "both roots behind" pre-filter, samples
-//     summed in min(4, spp) contiguous stripes then ((s0+s1)+s2)+s3.  The
-//     GPU output must equal this bit for bit.
+//     stackless throughput, exact "both roots behind" pre-filter, each
+//     sample's colour added to the pixel's integer sum in 2^-24 units
+//     (fix24; order-free), the pixel RN(float(sum)) * 2^-24 / spp.  The GPU
+//     output must equal this bit for bit.
 //
 //   MODE_REALM64 (3) — the reference's second namespace, realm.raytracing
 //     (src/realm/raytracing.clj, `clojure -M:realm`), in double: the same
@@ -297,6 +298,16 @@ struct Scene32 {
   const int* kind;
 };
 
+// A sample colour channel in the pixel's fixed-point sum (trace.hip fix24:
+// v_cvt_u32_f32 of c * 2^24 -- toward zero, NaN and c <= 0 -> 0, >= 2^32 ->
+// 2^32 - 1)
+inline uint32_t fix24(float c) {
+  const float v = c * 0x1p24f;
+  if (!(v > 0.0f)) return 0u;
+  if (v >= 0x1p32f) return 0xffffffffu;
+  return static_cast<uint32_t>(v);
+}
+
 void random_unit32(Rng& s, float& x, float& y, float& z) {
   float l2;
   do {
@@ -509,29 +520,24 @@ void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
         J.out64[o + 2] = res.z;
       }
     } else {
-      // contract: P = min(4, spp) contiguous sample stripes, each summed in
-      // sample order; total = ((s0 + s1) + s2) + s3; then / spp (trace.hip)
-      const int P = J.spp < 4 ? J.spp : 4;
-      const int q = J.spp / P, r = J.spp % P;
-      float tr_ = 0.0f, tg_ = 0.0f, tb_ = 0.0f;
+      // contract: each sample's colour channel becomes fix24(c) (c * 2^24
+      // toward zero, saturating; trace.hip's v_cvt_u32_f32) and the pixel
+      // sums them as integers (order-free); total = RN(float(sum)) * 2^-24,
+      // then / spp (realm: * RN(1/spp))
+      uint64_t sr = 0, sg = 0, sb = 0;
       const uint32_t pk = mix32(J.key ^ mix32(pixel));
-      int k = 0;
-      for (int sidx = 0; sidx < P; ++sidx) {
-        const int k_end = k + q + (sidx < r ? 1 : 0);
-        float ar = 0.0f, ag = 0.0f, ab = 0.0f;
-        for (; k < k_end; ++k) {
-          uint32_t st = mix32(pk + static_cast<uint32_t>(J.sample_begin + k) * 0x9e3779b9u);
-          if (st == 0) st = 0x6d2b79f5u;
-          float col[3];
-          sample32(J.s32, J.cam32, J.defocus, realm, px, gy, st, J.max_depth, col, segs);
-          ar += col[0];
-          ag += col[1];
-          ab += col[2];
-        }
-        tr_ += ar;
-        tg_ += ag;
-        tb_ += ab;
+      for (int k = 0; k < J.spp; ++k) {
+        uint32_t st = mix32(pk + static_cast<uint32_t>(J.sample_begin + k) * 0x9e3779b9u);
+        if (st == 0) st = 0x6d2b79f5u;
+        float col[3];
+        sample32(J.s32, J.cam32, J.defocus, realm, px, gy, st, J.max_depth, col, segs);
+        sr += fix24(col[0]);
+        sg += fix24(col[1]);
+        sb += fix24(col[2]);
       }
+      const float tr_ = static_cast<float>(sr) * 0x1p-24f;
+      const float tg_ = static_cast<float>(sg) * 0x1p-24f;
+      const float tb_ = static_cast<float>(sb) * 0x1p-24f;
       const float inv = static_cast<float>(J.spp);
       if (realm) {  // total * RN(1/spp)
         const float sc = 1.0f / inv;

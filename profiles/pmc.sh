@@ -3,19 +3,21 @@
 # rocprofv3 pass, kernel-trace + stats only (no sys/runtime traces), on the
 # bench's own command.  Usage (on the GPU box, from the repo root):
 #   profiles/pmc.sh gpurun_out/pmc [extra bench.py args]
-# Writes <out>/<pass>/prof_counter_collection.csv per pass.
+# Writes <out>/<pass>/prof_counter_collection.csv per pass, copied to
+# <out>/<pass>.csv (the form committed under profiles/rNN/ and read by bench.py).
 set -u
 OUT=${1:?outdir}; shift
 REPO=$PWD
 cd /tmp && export TMPDIR=/tmp && cd "$REPO" || exit 1
 mkdir -p "$OUT"
-BENCH=(python3 bench.py --cpu-baseline off --steps 2 --warmup 1 "$@")
+BENCH=(python3 bench.py --cpu-baseline off --e2e off --stats off --steps 2 --warmup 1 "$@")
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o prof \
     --pmc "$@" -- "${BENCH[@]}" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pass $name rc=$rc"
+  [ -f "$OUT/$name/prof_counter_collection.csv" ] && cp "$OUT/$name/prof_counter_collection.csv" "$OUT/$name.csv"
   case $rc in 124|134|137|139) echo "stopping: GPU step failed ($rc)"; exit $rc ;; esac
   return 0
 }

@@ -7,6 +7,12 @@
 //   write-color! src/raytracing.clj:19-26, PPM :172-175
 //   executor     src/raytracing.clj:157-171 (2 threads, contiguous chunks —
 //                here: N devices, interleaved 8-row tiles for balance)
+//
+// rt_render keeps, per device, the uploaded scenes (by content) and a few
+// render contexts (stream, device framebuffer, pinned staging buffer), so a
+// repeated call pays neither the upload and BVH builds nor the allocations,
+// and its launches reuse the stream whose adaptive tile order the previous
+// call recorded.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,6 +20,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -154,18 +162,155 @@ extern "C" const char* rt_version(void) { return "rtclj-mi355x 0.1 (gfx950)"; }
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// ---- per-device scene cache (content-keyed) ---------------------------------
+struct CachedScene {
+  uint64_t hash = 0;
+  std::vector<float> sphere, mat;
+  std::vector<int> kind;
+  std::shared_ptr<rt_dscene> ds;
+  uint64_t last_use = 0;
+};
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+  return h;
+}
+uint64_t scene_hash(const rt_scene& s) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  h = fnv1a(h, &s.n, sizeof s.n);
+  if (s.n > 0) {
+    h = fnv1a(h, s.sphere, sizeof(float) * 4 * s.n);
+    h = fnv1a(h, s.mat_kind, sizeof(int) * s.n);
+    h = fnv1a(h, s.mat, sizeof(float) * 4 * s.n);
+  }
+  return h;
+}
+bool same_scene(const CachedScene& c, const rt_scene& s) {
+  if (static_cast<int>(c.kind.size()) != s.n) return false;
+  if (s.n == 0) return true;
+  return std::memcmp(c.sphere.data(), s.sphere, sizeof(float) * 4 * s.n) == 0 &&
+         std::memcmp(c.kind.data(), s.mat_kind, sizeof(int) * s.n) == 0 &&
+         std::memcmp(c.mat.data(), s.mat, sizeof(float) * 4 * s.n) == 0;
+}
+
+// ---- per-device render context: stream, buffers, events ---------------------
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  float* d_out = nullptr;
+  size_t d_cap = 0;           // floats
+  float* h_pin = nullptr;     // pinned staging for the D2H
+  size_t h_cap = 0;           // floats
+  uint64_t* d_cnt = nullptr;
+  uint64_t* h_cnt = nullptr;  // pinned
+  ~Ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e2) (void)hipEventDestroy(e2);
+    if (d_out) (void)hipFree(d_out);
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (h_pin) (void)hipHostFree(h_pin);
+    if (h_cnt) (void)hipHostFree(h_cnt);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+constexpr int kSceneCache = 4;   // scenes kept per device (least recently used out)
+constexpr int kFreeCtx = 4;      // idle contexts kept per device
+
+struct DeviceCache {
+  std::mutex mu;
+  std::vector<CachedScene> scenes;
+  std::vector<std::unique_ptr<Ctx>> free_ctx;
+  uint64_t tick = 0;
+};
+// never destroyed: HIP may already be torn down when static destructors run
+std::vector<DeviceCache>* g_cache = new std::vector<DeviceCache>(64);
+std::mutex g_cache_mu;
+
+// the cached device scene of s on `device`, uploading it on a miss
+int get_scene(int device, const rt_scene* s, std::shared_ptr<rt_dscene>* out, bool* hit) {
+  DeviceCache& dc = (*g_cache)[device];
+  const uint64_t h = scene_hash(*s);
+  {
+    std::lock_guard<std::mutex> lk(dc.mu);
+    for (CachedScene& c : dc.scenes)
+      if (c.hash == h && same_scene(c, *s)) {
+        c.last_use = ++dc.tick;
+        *out = c.ds;
+        *hit = true;
+        return RT_OK;
+      }
+  }
+  rt_dscene* raw = nullptr;
+  const int rc = rt_scene_upload(device, s, &raw);
+  if (rc != RT_OK) return rc;
+  std::shared_ptr<rt_dscene> ds(raw, [](rt_dscene* d) { rt_scene_free(d); });
+  CachedScene c;
+  c.hash = h;
+  if (s->n > 0) {
+    c.sphere.assign(s->sphere, s->sphere + 4 * s->n);
+    c.kind.assign(s->mat_kind, s->mat_kind + s->n);
+    c.mat.assign(s->mat, s->mat + 4 * s->n);
+  }
+  c.ds = ds;
+  std::lock_guard<std::mutex> lk(dc.mu);
+  c.last_use = ++dc.tick;
+  if (static_cast<int>(dc.scenes.size()) >= kSceneCache) {
+    auto lru = std::min_element(dc.scenes.begin(), dc.scenes.end(),
+                                [](const CachedScene& x, const CachedScene& y) { return x.last_use < y.last_use; });
+    dc.scenes.erase(lru);   // freed when the last in-flight render drops it
+  }
+  dc.scenes.push_back(std::move(c));
+  *out = ds;
+  *hit = false;
+  return RT_OK;
+}
+
+std::unique_ptr<Ctx> take_ctx(int device) {
+  DeviceCache& dc = (*g_cache)[device];
+  {
+    std::lock_guard<std::mutex> lk(dc.mu);
+    if (!dc.free_ctx.empty()) {
+      std::unique_ptr<Ctx> c = std::move(dc.free_ctx.back());
+      dc.free_ctx.pop_back();
+      return c;
+    }
+  }
+  auto c = std::make_unique<Ctx>();
+  c->device = device;
+  return c;
+}
+void give_ctx(std::unique_ptr<Ctx> c) {
+  DeviceCache& dc = (*g_cache)[c->device];
+  std::lock_guard<std::mutex> lk(dc.mu);
+  if (static_cast<int>(dc.free_ctx.size()) < kFreeCtx) dc.free_ctx.push_back(std::move(c));
+}
+
 struct Shard {
   int device = 0;
   rt_params p{};
   int rows = 0;
-  std::vector<float> host;
   int status = RT_OK;
   std::string err;
   uint64_t counters[2] = {0, 0};
   float ms = 0.0f;
+  double upload_ms = 0.0, gather_ms = 0.0;
+  bool cached = false;
 };
 
-void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh) {
+// one device's share: scene (cached), launch, D2H into pinned staging, then
+// the host scatter of its compacted row tiles into out_rgb (disjoint rows:
+// the shards scatter in parallel, each as soon as its own device is done)
+void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb, int rows_total, int ntiles,
+               int nshards, int shard_idx) {
   auto fail = [&](int code) {
     sh->status = code;
     sh->err = rt_last_error();
@@ -174,60 +319,111 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh) {
     sh->status = RT_E_HIP;
     sh->err = std::string(what) + ": " + hipGetErrorString(e);
   };
-  rt_dscene* ds = nullptr;
-  int rc = rt_scene_upload(sh->device, s, &ds);
+  const auto t0 = Clock::now();
+  std::shared_ptr<rt_dscene> ds;
+  int rc = get_scene(sh->device, s, &ds, &sh->cached);
   if (rc != RT_OK) return fail(rc);
-  float* d_out = nullptr;
-  uint64_t* d_cnt = nullptr;
-  hipStream_t stream = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  sh->upload_ms = ms_since(t0);
+  std::unique_ptr<Ctx> cx = take_ctx(sh->device);
   const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
-  hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc(&d_out, std::max<size_t>(nfl, 1) * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&d_cnt, 2 * sizeof(uint64_t));
-  if (e == hipSuccess) e = hipMemsetAsync(d_cnt, 0, 2 * sizeof(uint64_t), stream);
-  if (e == hipSuccess) e = hipEventCreate(&e0);
-  if (e == hipSuccess) e = hipEventCreate(&e1);
-  if (e == hipSuccess) e = hipEventRecord(e0, stream);
+  hipError_t e = hipSetDevice(sh->device);
+  if (e == hipSuccess && !cx->stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess && !cx->e0) e = hipEventCreate(&cx->e0);
+  if (e == hipSuccess && !cx->e1) e = hipEventCreate(&cx->e1);
+  if (e == hipSuccess && !cx->e2) e = hipEventCreate(&cx->e2);
+  if (e == hipSuccess && !cx->d_cnt) e = hipMalloc(&cx->d_cnt, 2 * sizeof(uint64_t));
+  if (e == hipSuccess && !cx->h_cnt) e = hipHostMalloc(&cx->h_cnt, 2 * sizeof(uint64_t), hipHostMallocDefault);
+  if (e == hipSuccess && cx->d_cap < nfl) {
+    if (cx->d_out) (void)hipFree(cx->d_out);
+    cx->d_out = nullptr;
+    cx->d_cap = 0;
+    e = hipMalloc(&cx->d_out, std::max<size_t>(nfl, 1) * sizeof(float));
+    if (e == hipSuccess) cx->d_cap = nfl;
+  }
+  if (e == hipSuccess && cx->h_cap < nfl) {
+    if (cx->h_pin) (void)hipHostFree(cx->h_pin);
+    cx->h_pin = nullptr;
+    cx->h_cap = 0;
+    e = hipHostMalloc(&cx->h_pin, std::max<size_t>(nfl, 1) * sizeof(float), hipHostMallocDefault);
+    if (e == hipSuccess) cx->h_cap = nfl;
+  }
+  if (e == hipSuccess) e = hipMemsetAsync(cx->d_cnt, 0, 2 * sizeof(uint64_t), cx->stream);
+  if (e == hipSuccess) e = hipEventRecord(cx->e0, cx->stream);
   if (e != hipSuccess) {
     hip_fail(e, "rt_render setup");
   } else {
-    rc = rt_launch(ds, c, &sh->p, d_out, d_cnt, stream);
+    rc = rt_launch(ds.get(), c, &sh->p, cx->d_out, cx->d_cnt, cx->stream);
     if (rc != RT_OK) {
       fail(rc);
     } else {
-      e = hipEventRecord(e1, stream);
-      sh->host.resize(nfl);
+      e = hipEventRecord(cx->e1, cx->stream);
       if (e == hipSuccess && nfl)
-        e = hipMemcpyAsync(sh->host.data(), d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, stream);
+        e = hipMemcpyAsync(cx->h_pin, cx->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, cx->stream);
       if (e == hipSuccess)
-        e = hipMemcpyAsync(sh->counters, d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream);
-      if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, e0, e1);
-      if (e != hipSuccess) hip_fail(e, "rt_render trace/gather");
+        e = hipMemcpyAsync(cx->h_cnt, cx->d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, cx->stream);
+      if (e == hipSuccess) e = hipEventRecord(cx->e2, cx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(cx->stream);
+      float d2h = 0.0f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, cx->e0, cx->e1);
+      if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->e1, cx->e2);
+      if (e != hipSuccess) {
+        hip_fail(e, "rt_render trace/gather");
+      } else {
+        sh->counters[0] = cx->h_cnt[0];
+        sh->counters[1] = cx->h_cnt[1];
+        // host scatter: compacted tiles back to their image rows
+        const auto ts = Clock::now();
+        const size_t rowf = static_cast<size_t>(sh->p.width) * 3;
+        if (nshards == 1) {
+          std::memcpy(out_rgb, cx->h_pin, nfl * sizeof(float));
+        } else {
+          const int T = sh->p.row_tile;
+          int ro = 0;
+          for (int t = shard_idx; t < ntiles; t += nshards) {
+            const int r0 = t * T, nr = std::min(T, rows_total - r0);
+            std::memcpy(out_rgb + static_cast<size_t>(r0) * rowf, cx->h_pin + static_cast<size_t>(ro) * rowf,
+                        nr * rowf * sizeof(float));
+            ro += nr;
+          }
+        }
+        sh->gather_ms = d2h + ms_since(ts);
+      }
     }
   }
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  if (d_out) (void)hipFree(d_out);
-  if (d_cnt) (void)hipFree(d_cnt);
-  if (stream) (void)hipStreamDestroy(stream);
-  rt_scene_free(ds);
+  if (sh->status == RT_OK) give_ctx(std::move(cx));
 }
 
 }  // namespace
 
+extern "C" int rt_cache_clear(void) {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  int dropped = 0;
+  for (DeviceCache& dc : *g_cache) {
+    std::vector<CachedScene> scenes;
+    std::vector<std::unique_ptr<Ctx>> ctxs;
+    {
+      std::lock_guard<std::mutex> l2(dc.mu);
+      scenes.swap(dc.scenes);
+      ctxs.swap(dc.free_ctx);
+    }
+    dropped += static_cast<int>(scenes.size());
+  }
+  return dropped;
+}
+
 extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p, float* out_rgb,
                          size_t out_len, rt_stats* stats) {
   clear_error();
-  const auto t0 = std::chrono::steady_clock::now();
+  const auto t0 = Clock::now();
   if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, "rt_render: NULL argument");
   const bool on_dev0 = (p->flags & RT_FLAG_SHARDS_ON_DEVICE0) != 0;
-  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->n_devices < 0 ||
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP || p->n_devices < 0 ||
       (p->flags & ~(RT_FLAG_SHARDS_ON_DEVICE0 | RT_FLAG_REALM)) != 0 || (on_dev0 && p->n_devices == 0))
     return set_error(RT_E_ARG, "rt_render: bad width/height/spp/flags/n_devices");
   if (p->tile_step != 0 || p->tile_first != 0)
     return set_error(RT_E_ARG, "rt_render: tile_first/tile_step are per-shard (rt_launch) fields");
+  if (s->n < 0 || (s->n > 0 && (!s->sphere || !s->mat_kind || !s->mat)))
+    return set_error(RT_E_ARG, "rt_render: bad scene arrays");
   const int rows = rows_out(*p);
   if (rows < 0) return set_error(RT_E_ARG, "rt_render: bad row range");
   const size_t need = static_cast<size_t>(rows) * p->width * 3;
@@ -239,9 +435,11 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   if (ndev > ndev_vis && !on_dev0)
     return set_error(RT_E_NODEV, "rt_render: n_devices " + std::to_string(ndev) + " > visible " +
                                      std::to_string(ndev_vis));
+  if (ndev_vis > static_cast<int>(g_cache->size()))
+    return set_error(RT_E_NODEV, "rt_render: more than 64 devices");
   const int T = p->row_tile > 0 ? p->row_tile : 8;
   const int ntiles = (rows + T - 1) / T;
-  ndev = std::max(1, std::min(ndev, ntiles));
+  ndev = std::max(1, std::min(ndev, std::max(ntiles, 1)));
 
   std::vector<Shard> shards(ndev);
   for (int d = 0; d < ndev; ++d) {
@@ -257,31 +455,23 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     sh.rows = rows_out(sh.p);
   }
   if (ndev == 1) {
-    run_shard(s, c, &shards[0]);
+    run_shard(s, c, &shards[0], out_rgb, rows, ntiles, 1, 0);
   } else {
     std::vector<std::thread> th;
-    for (int d = 0; d < ndev; ++d) th.emplace_back(run_shard, s, c, &shards[d]);
+    for (int d = 0; d < ndev; ++d) th.emplace_back(run_shard, s, c, &shards[d], out_rgb, rows, ntiles, ndev, d);
     for (auto& t : th) t.join();
   }
-  double kms = 0;
+  double kms = 0, ksum = 0, ums = 0, gms = 0;
   uint64_t segs = 0, smp = 0;
+  int cached = 0;
   for (int d = 0; d < ndev; ++d) {
     Shard& sh = shards[d];
     if (sh.status != RT_OK) return set_error(sh.status, "device " + std::to_string(d) + ": " + sh.err);
-    // host-side gather: compacted tiles back to their image rows
-    const size_t rowf = static_cast<size_t>(p->width) * 3;
-    if (ndev == 1) {
-      std::memcpy(out_rgb, sh.host.data(), sh.host.size() * sizeof(float));
-    } else {
-      int ro = 0;
-      for (int t = d; t < ntiles; t += ndev) {
-        const int r0 = t * T, nr = std::min(T, rows - r0);
-        std::memcpy(out_rgb + static_cast<size_t>(r0) * rowf, sh.host.data() + static_cast<size_t>(ro) * rowf,
-                    nr * rowf * sizeof(float));
-        ro += nr;
-      }
-    }
     kms = std::max(kms, static_cast<double>(sh.ms));
+    ksum += sh.ms;
+    ums = std::max(ums, sh.upload_ms);
+    gms = std::max(gms, sh.gather_ms);
+    cached += sh.cached ? 1 : 0;
     segs += sh.counters[0];
     smp += sh.counters[1];
   }
@@ -289,8 +479,12 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     stats->segments = segs;
     stats->samples = smp;
     stats->kernel_ms = kms;
-    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    stats->kernel_ms_mean = ksum / ndev;
+    stats->upload_ms = ums;
+    stats->gather_ms = gms;
+    stats->scene_cached = cached;
     stats->n_devices = ndev;
+    stats->total_ms = ms_since(t0);
   }
   return RT_OK;
 }

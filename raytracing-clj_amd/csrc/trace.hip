@@ -8,31 +8,35 @@
 //   lambertian / metal / dielectric   src/material.clj:13-46
 //   vec3a math, rand samplers         src/vec3a.clj:56-101
 //
-// Execution shape (MI355X / CDNA4):
-//   * one lane = one pixel; one wave = an 8x8 pixel tile (ray coherence for
-//     camera rays); one 256-thread workgroup = 16x16 pixels;
-//   * the lane runs its spp samples back to back with *sample regeneration*:
-//     when a path ends (sky / absorbed / depth) the lane accumulates and
-//     starts its next camera sample in the same loop iteration structure, so
-//     a wave keeps all 64 lanes busy until its pixels run out of samples;
+// Execution shape (MI355X / CDNA4), DESIGN.md §3:
+//   * one 256-thread workgroup owns an 8x8 pixel tile and every
+//     (pixel, sample) pair of it: the *sample pool*.  A lane runs one path
+//     at a time; when it ends (sky / absorbed / depth) the lane hands in its
+//     colour and takes the next pair from an LDS counter, so no lane idles
+//     until the pool is empty;
 //   * ray-color's recursion becomes a throughput accumulator T (stackless);
-//   * the sphere table (centre, -r^2: 16 B per body) is staged once per
-//     workgroup in LDS (variant 1) or read through the scalar cache into
-//     SGPRs (variant 2); the hit test loop is wave-uniform (every lane scans
-//     every body in order), only the rare "line meets sphere" block diverges;
+//   * the closest hit comes from a BVH in LDS (default) or, in the fallback
+//     and diagnostic variants, a linear scan of the sphere table (LDS or the
+//     scalar cache); either way it is the hit the reference's linear scan
+//     returns, bit for bit;
 //   * per-lane xorshift32 RNG, seeded per (seed, pixel, sample) by a hash;
-//   * the framebuffer is written once per pixel (fp32 RGB, 12 B).
+//   * a finished sample's colour is added to its pixel's fixed-point sum in
+//     LDS (u64, 2^-24 units): integer addition, so the total does not depend
+//     on the order in which samples finish, and nothing goes through HBM but
+//     the scene and the framebuffer, written once per pixel (fp32 RGB).
 //
 // Arithmetic contract (fp32; mirrored op-for-op by the oracle's fp32 mode,
 // oracle/rt_oracle.cpp, so GPU and CPU agree bit-for-bit): every fused
 // multiply-add is an explicit fmaf, the file is compiled with
 // -ffp-contract=off, division and sqrt are IEEE correctly rounded (HIP's
 // default), normalisations multiply by one correctly rounded reciprocal
-// (d * (1/|d|), (p - C) * (1/r)), and no transcendental function is used.
+// (d * (1/|d|), (p - C) * (1/r)), no transcendental function is used, and a
+// pixel is RN(RN(float(sum of fix24(sample colour))) * 2^-24 / spp).
 // See DESIGN.md §3.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -56,8 +60,7 @@ struct alignas(16) KArgs {
   const int* kind;     // n: material kind
   float* out;          // rows_out x width x 3
   unsigned long long* counters;  // NULL or [segments, samples]
-  unsigned long long* dbg;       // stats build only: [wave iters, active lanes, sphere iters,
-                                 //  candidate blocks, lanes in blocks, waves]
+  unsigned long long* dbg;       // stats build only: event counters (rt_debug_stats)
   unsigned long long* dbgw;      // stats build only: per wave {t_start, t_end, hw_id, xcc_id}
   float cam[18];       // center, p00, du, dv, disk_u, disk_v
   int defocus;
@@ -66,7 +69,7 @@ struct alignas(16) KArgs {
   int width;
   int rows_out;
   int row_begin, row_tile, tile_first, tile_step;
-  // BVH traversal (SCAN_BVH): blob = nodes | pairs | pidx (the LDS image)
+  // BVH traversal: blob = nodes | pairs | pidx (the LDS image)
   const float4* bvh_blob;
   int bvh_blob_f4;       // blob size in float4
   int bvh_off_pairs;     // byte offsets inside the blob
@@ -77,10 +80,8 @@ struct alignas(16) KArgs {
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
   unsigned* tile_cost;     // nullable: per tile, the longest of its waves' durations (s_memrealtime ticks)
-  float* pool_scratch;     // sample pool (LPP < 0): per pool, [pixel][pool_chunk samples][rgb], then the lanes' sums
-  int pool_chunk;          // samples per pixel per pool round (one launch per round)
-  int pool_c0;             // this launch's round starts at sample pool_c0 of each pixel
   int spp, sample_begin, max_depth;
+  uint32_t spp_magic;    // ceil(2^32 / spp) for j / spp by multiply-high (0: spp == 1 or too large)
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
 };
@@ -129,28 +130,43 @@ __device__ __forceinline__ float rng_sym(uint32_t& s) {
   return fmaf(static_cast<float>(s >> 8), 0x1p-23f, -1.0f);
 }
 
-// vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
-// 0 < |v|^2 <= 1 (1e-160 underflows to 0 in fp32), then v / |v|.
 // stats builds: count one event per wave (by its first active lane)
 __device__ __forceinline__ void wave_event(uint64_t& c) {
   const uint64_t ex = __builtin_amdgcn_read_exec();
   if ((threadIdx.x & 63) == static_cast<unsigned>(__ffsll(static_cast<long long>(ex)) - 1)) ++c;
 }
 
+// vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
+// 0 < |v|^2 <= 1 (1e-160 underflows to 0 in fp32), then v / |v|.
 template <bool STATS = false>
-__device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z, uint64_t* trips = nullptr) {
+__device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z, uint64_t* trips = nullptr,
+                                            uint64_t* flops = nullptr) {
   float l2;
   do {
-    if constexpr (STATS) wave_event(*trips);
+    if constexpr (STATS) {
+      wave_event(*trips);
+      *flops += 11;   // 3 x (2 xi - 1) + |v|^2
+    }
     x = rng_sym(s);
     y = rng_sym(s);
     z = rng_sym(s);
     l2 = fmaf(z, z, fmaf(y, y, x * x));
   } while (!(l2 > 0.0f && l2 <= 1.0f));
   const float il = 1.0f / sqrt_rn(l2);   // contract: v * (1/|v|)
+  if constexpr (STATS) *flops += 5;
   x = x * il;
   y = y * il;
   z = z * il;
+}
+
+// A sample's colour channel in the pixel's fixed-point sum: c * 2^24
+// converted by v_cvt_u32_f32 (toward zero; NaN and c <= 0 give 0, c >= 256
+// gives 2^32 - 1).  The sums are integers, so any completion order gives
+// the same total (oracle: fix24).
+__device__ __forceinline__ uint32_t fix24(float c) {
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(c * 0x1p24f));
+  return r;
 }
 
 // stats build only: shader-clock stamp (s_memtime, drains lgkm; diagnostic)
@@ -193,93 +209,61 @@ struct alignas(16) KNode {
 };
 static_assert(sizeof(KNode) == 80, "KNode layout");
 
-// Sample stripes (arithmetic contract): a pixel's spp samples are split into
-// P = min(4, spp) contiguous stripes (stripe s: samples [s*q + min(s,r),
-// +q + (s<r)), q = spp/P, r = spp%P); each stripe is summed sequentially in
-// sample order, and the pixel total is ((s0 + s1) + s2) + s3, then / spp.
-// LPP lanes work on one pixel (1, 2 or 4; LPP > 1 needs P == 4): lane group
-// g runs stripes [g*4/LPP, (g+1)*4/LPP) back to back; the groups' stripe sums
-// are combined in stripe order after the loop (cross-lane), so every LPP
-// gives the same bits.  A wave covers 64/LPP pixels (8x8, 8x4 or 4x4).
-__device__ __forceinline__ int stripe_begin(int s, int spp, int P) {
-  const int q = spp / P, r = spp % P;
-  return s * q + (s < r ? s : r);
-}
+// The pool tile: 8 x 8 pixels per 256-thread workgroup
+constexpr int kTile = 8;
+constexpr int kPoolPx = kTile * kTile;
 
-template <int SRC, int SCAN, int LPP, bool STATS = false>
+template <int SRC, int SCAN, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
-  static_assert(LPP == -3 || LPP == -2 || LPP == -1 || LPP == 1 || LPP == 2 || LPP == 4,
-                "lanes per pixel (< 0: sample pool)");
-  // LPP -1 / -2 = the sample pool: a wave owns a 4 x 4 / 8 x 8 pixel tile and
-  // the tile's pixel x sample pairs; a lane whose path ends takes the next
-  // pair, so no lane idles until the pool is empty.  Each sample's colour goes
-  // to the wave's scratch; after the pool, lane (pixel, stripe) (4 x 4) or
-  // lane = pixel (8 x 8) adds the samples in sample order, stripe by stripe:
-  // the stripe contract of LPP 4 / 1, same bits.  LPP -3: one pool per
-  // workgroup, its 8 x 8 pixels shared by the 4 waves (refills through an LDS
-  // counter), so the waves of a workgroup finish together; each wave sums 16
-  // of the pixels as LPP -1 does.
-  constexpr bool POOL = LPP < 0;
-  constexpr bool WGP = LPP == -3;
-  constexpr int LPPE = (LPP == -1 || LPP == -3) ? 4 : LPP == -2 ? 1 : LPP;
-  constexpr int PPX = (LPP == -2 || LPP == -3) ? 64 : 16;   // pixels of one pool
-  static_assert(!WGP || (SRC == SRC_LDS && is_bvh_scan(SCAN)), "workgroup pool: LDS BVH variants");
-  __shared__ int s_pool_next;   // WGP: the workgroup pool's next free index
+  // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
+  // indices j in [0, npx * spp), pixel-major (j -> pixel j / spp, sample
+  // j % spp: the lanes in flight hold consecutive samples of a few pixels,
+  // the most coherent rays a workgroup can hold).  Lanes start on j = 0..255;
+  // a lane whose path ends takes the next index from an LDS counter (one
+  // ds_add per wave event, then an mbcnt prefix).  The colour sums are u64
+  // per pixel and channel in LDS, added with ds_add_u64: order-free.
+  __shared__ int s_pool_next;
+  __shared__ unsigned long long s_acc[kPoolPx * 3];
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
   uint64_t st_ball = 0, st_disk = 0;          // wave-level rejection-loop trips (random-unit, disk)
+  uint64_t st_fl = 0;                         // executed fp32 flops of this lane (fma = 2)
+  uint64_t st_fresh = 0, st_fresh_lanes = 0;  // wave-level camera-sample blocks, lanes in them
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if (STATS || a.tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if constexpr (is_bvh_scan(SCAN)) {
-    if constexpr (SRC == SRC_LDS) {
-      if (WGP && threadIdx.x == 0) s_pool_next = 256;   // (published by the barrier below)
+  if (threadIdx.x == 0) s_pool_next = 256;
+  if (threadIdx.x < kPoolPx * 3) s_acc[threadIdx.x] = 0ull;
+  if constexpr (SRC == SRC_LDS) {
+    if constexpr (is_bvh_scan(SCAN)) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
-      __syncthreads();
+    } else {
+      const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
+      for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
     }
-  } else if constexpr (SRC == SRC_LDS) {
-    const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
-    for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
-    __syncthreads();
   }
+  __syncthreads();
   // BVH traversal stack: bvh_stack node refs per lane, [entry][lane] (no bank conflicts)
   // (u8 entries for the 8-body-leaf traversal, whose trees the host caps at
-  // 256 nodes: with its u16 body indices this keeps a 1025-body scene's
+  // 256 nodes: with its u16 body indices this keeps a 1000-body scene's
   // image under the 32 KB that 5 workgroups per CU allow)
   using StackT = std::conditional_t<SCAN == SCAN_BVHO, unsigned char, unsigned short>;
   StackT* s_stack = reinterpret_cast<StackT*>(
       reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
 
-  // lane -> (pixel, stripe group): a wave owns a TW x TH pixel tile
-  // (PX = 64/LPP pixels), lane group grp = lane / PX; the block's 4 waves
-  // tile 2 x 2.
-  constexpr int PX = 64 / LPPE;
-  constexpr int TW = (LPPE == 4) ? 4 : 8;
-  constexpr int TH = (LPPE == 1) ? 8 : 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int lane = threadIdx.x & 63;
-  const int pl = lane % PX;     // pixel within the wave tile
-  const int grp = lane / PX;    // stripe group
   // the block's tile: its dispatch slot, or the tile_order permutation of it
   const int slot = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
   const int tile = a.tile_order ? a.tile_order[slot] : slot;
   const int tbx = tile % static_cast<int>(gridDim.x), tby = tile / static_cast<int>(gridDim.x);
-  const int x0 = tbx * (2 * TW) + (wave & 1) * TW;   // the wave's tile
-  const int y0 = tby * (2 * TH) + (wave >> 1) * TH;
-  // pool: the pool tile's in-image part, vw x vh pixels, pixel q at
-  // (q % vw, q / vw); the pool tile is the wave's, or (WGP) the workgroup's
-  const int qx0 = WGP ? tbx * 8 : x0, qy0 = WGP ? tby * 8 : y0;
-  const int vw = POOL ? max(0, min(WGP ? 8 : TW, a.width - qx0)) : TW;
-  const int vh = POOL ? max(0, min(WGP ? 8 : TH, a.rows_out - qy0)) : TH;
+  // the tile's in-image part, vw x vh pixels; pool pixel q at (q % vw, q / vw)
+  const int qx0 = tbx * kTile, qy0 = tby * kTile;
+  const int vw = max(0, min(kTile, a.width - qx0));
+  const int vh = max(0, min(kTile, a.rows_out - qy0));
   const int npx = vw * vh;
-  const int fp = WGP ? wave * 16 + pl : pl;   // the pool pixel this lane sums (and writes)
-  int px = POOL ? qx0 + (vw > 0 ? fp % vw : 0) : x0 + (pl % TW);
-  int ro = POOL ? qy0 + (vw > 0 ? fp / vw : 0) : y0 + (pl / TW);
-  const bool in_image = POOL ? (fp < npx) : (px < a.width) && (ro < a.rows_out);
-  bool active = in_image;
 
   // compacted output row -> global image row (interleaved row tiles)
   auto image_row = [&](int r) {
@@ -292,37 +276,17 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   auto pixel_key = [&](int x, int y) {
     return mix32(a.key ^ mix32(static_cast<uint32_t>(y) * static_cast<uint32_t>(a.width) + static_cast<uint32_t>(x)));
   };
-  int gy = image_row(ro);
-
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
-  uint32_t pkey = pixel_key(px, gy);
-
-  // this lane's samples [k, k_end) = stripes [grp*SPL, (grp+1)*SPL)
-  const int P = a.spp < 4 ? (a.spp > 0 ? a.spp : 1) : 4;
-  constexpr int SPL = 4 / LPPE;  // stripes per lane (LPP > 1 requires P == 4)
-  int k = LPPE == 1 ? 0 : stripe_begin(grp * SPL, a.spp, P);
-  const int k_end = LPPE == 1 ? a.spp : stripe_begin(grp * SPL + SPL, a.spp, P);
-  int stripe = LPPE == 1 ? 0 : grp * SPL;            // current stripe index
-  int k_next = stripe_begin(stripe + 1, a.spp, P);   // its end
-  float accr = 0.0f, accg = 0.0f, accb = 0.0f;       // current stripe sum
-  float totr = 0.0f, totg = 0.0f, totb = 0.0f;       // LPP == 1: running total
-  float s0r = 0.0f, s0g = 0.0f, s0b = 0.0f;          // LPP == 2: the lane's first stripe sum
   uint32_t segs = 0;
-  if (!POOL && (a.spp <= 0 || a.max_depth <= 0 || k >= k_end)) active = false;  // depth<=0 -> black (:46-47)
 
-  // pool state: round [c0, c0 + cn) of each pixel's samples; pool index j ->
-  // (pixel j / cn, sample c0 + j % cn); the next free index is `base`
-  // the pool's scratch: PPX pixels x pool_chunk samples x rgb, then the
-  // lanes' sums between rounds (total and current stripe, rgb each)
-  float* const scr = POOL ? a.pool_scratch + (WGP ? static_cast<size_t>(tile) : static_cast<size_t>(tile) * 4 + wave) *
-                                                 (static_cast<size_t>(PPX * 3) * a.pool_chunk + (WGP ? 256 : 64) * 6)
-                          : nullptr;
-  int c0 = 0, cn = 0, pool = 0, j = WGP ? static_cast<int>(threadIdx.x) : lane, base = 64, q = 0;
-  const bool pool_work = a.spp > 0 && a.max_depth > 0 && npx > 0;
-  // j / cn and q / vw by multiply-high: exact while j * cn < 2^32, i.e.
-  // 16 * cn^2 < 2^32 (the host caps cn at 16384); divisor 1 is special-cased
+  // pool index j -> (pixel q = j / spp, sample k = j % spp); the next free
+  // index is `base`.  j / spp by multiply-high: exact while j * spp < 2^32,
+  // i.e. 64 * spp^2 < 2^32 (the host passes spp_magic = 0 above 8191 and for
+  // spp = 1); q / vw likewise (q < 64, vw <= 8)
+  const int pool = (a.spp > 0 && a.max_depth > 0) ? npx * a.spp : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
-  uint32_t mag_cn = 0;
+  int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
+  bool active = j < pool;
 
   // path state
   uint32_t st = 0;
@@ -332,13 +296,6 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   int last = -1;   // body the current ray leaves (-1: camera ray)
   bool fresh = true;
 
-  if constexpr (POOL) {   // this launch's round: samples [c0, c0 + cn) of every pixel
-    c0 = a.pool_c0;
-    cn = min(a.pool_chunk, a.spp - c0);
-    pool = pool_work ? npx * cn : 0;
-    mag_cn = cn > 0 ? 0xffffffffu / static_cast<uint32_t>(cn) + 1u : 0u;
-    active = j < pool;
-  }
   while (active) {
     if constexpr (STATS) st_ts = stamp();
     if constexpr (STATS) {  // counted once per wave event, by its first active lane
@@ -349,19 +306,22 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       }
     }
     if (fresh) {
-      if constexpr (POOL) {   // pool index -> (pixel, sample)
-        // pixel-major: the lanes in flight hold consecutive samples of one or
-        // two pixels (the most coherent rays; 1-2 % faster than pixel-minor)
-        q = cn == 1 ? j : static_cast<int>(__umulhi(static_cast<uint32_t>(j), mag_cn));
-        k = c0 + (j - q * cn);
-        const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
-        px = qx0 + (q - qy * vw);
-        ro = qy0 + qy;
-        gy = image_row(ro);
-        pkey = pixel_key(px, gy);
+      if constexpr (STATS) {
+        const uint64_t ex = __builtin_amdgcn_read_exec();
+        if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+          ++st_fresh;
+          st_fresh_lanes += __popcll(ex);
+        }
       }
+      // pool index -> (pixel, sample)
+      if (a.spp_magic) q = static_cast<int>(__umulhi(static_cast<uint32_t>(j), a.spp_magic));
+      else q = a.spp == 1 ? j : static_cast<int>(static_cast<uint32_t>(j) / static_cast<uint32_t>(a.spp));
+      k = j - q * a.spp;
+      const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
+      const int px = qx0 + (q - qy * vw);
+      const int gy = image_row(qy0 + qy);
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
-      st = mix32(pkey + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
+      st = mix32(pixel_key(px, gy) + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
       // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
       const float fx = static_cast<float>(px) + rng_centered(st);
@@ -371,20 +331,25 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
       if (a.defocus) {
         // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
-        float qx, qy;
+        float qx, qy2;
         do {
-          if constexpr (STATS) wave_event(st_disk);
+          if constexpr (STATS) {
+            wave_event(st_disk);
+            st_fl += 7;   // 2 x (2 xi - 1) + |q|^2
+          }
           qx = rng_sym(st);
-          qy = rng_sym(st);
-        } while (!(fmaf(qy, qy, qx * qx) < 1.0f));
-        ox = fmaf(a.cam[15], qy, fmaf(a.cam[12], qx, cx));
-        oy = fmaf(a.cam[16], qy, fmaf(a.cam[13], qx, cy));
-        oz = fmaf(a.cam[17], qy, fmaf(a.cam[14], qx, cz));
+          qy2 = rng_sym(st);
+        } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        if constexpr (STATS) st_fl += 12;
+        ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
+        oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
+        oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
       } else {
         ox = cx;
         oy = cy;
         oz = cz;
       }
+      if constexpr (STATS) st_fl += 21;   // jitter 2 x (fma + add), sample point 3 x 2 fma, d = s - o
       dx = sx - ox;
       dy = sy - oy;
       dz = sz - oz;
@@ -393,6 +358,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       last = -1;
       fresh = false;
     }
+
 
     if constexpr (STATS) {
       const uint64_t t = stamp();
@@ -406,12 +372,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     const float il = 1.0f / len;                              // vec3a/unit as d * (1/|d|)
     const float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
+    if constexpr (STATS) st_fl += 11;                         // |d|, 1/|d|, u, t-min
     float best_t = INFINITY;
     int best = -1;
     // the candidate block: roots, root choice, strict closest test.  The body
     // the ray is leaving gets sq = |h| (exact arithmetic has c = 0 there:
     // the origin lies on its surface) -- the self-hit acne guard.
     auto consider = [&](float h, float disc, int s) {
+      if constexpr (STATS) st_fl += 3;
       if constexpr (STATS) {
         const uint64_t ex = __builtin_amdgcn_read_exec();
         if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -454,6 +422,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       //    padded interval misses (tmin, best_t].
       // branch-free acceptance (bitwise predicates: no exec-mask blocks)
       auto consider_tie = [&](float h, float disc, int s) {
+        if constexpr (STATS) st_fl += 3;   // sqrt, h -/+ sq
         if constexpr (STATS) ++st_blk_lanes;
         const float sq = (s == last) ? fabsf(h) : sqrt_rn(disc);
         const float tn = h - sq;
@@ -485,6 +454,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float ecx = ox - a.bvh_c[0], ecy = oy - a.bvh_c[1], ecz = oz - a.bvh_c[2];
       const float D = __builtin_amdgcn_sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
       const float P = fmaf(2e-3f, D, 1e-6f);
+      if constexpr (STATS) st_fl += 27;   // o - c, D, P, 3 rcp, 6 slab offsets
       // |u| >= 1e-24 keeps 1/u finite: with u = 0 an infinite 1/u makes the
       // fma bounds NaN and -inf, which would collapse the slab (a false miss);
       // finite, the slab of an origin inside the padded box spans ~+-1e24 and
@@ -529,6 +499,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const PidxT* const li = pidx + p;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
+          if constexpr (STATS) st_fl += 32;   // 2 bodies x (oc 3, h 5, c 6, disc 2)
           const Pair g = lp[hb + q];
           const PidxT id = li[hb + q];
           const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
@@ -593,6 +564,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // (the near plane's t is the min of the two planes' t, bit for bit: the
       // same fma on the same operands -- no min/max orders them)
       auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
+        if constexpr (STATS) st_fl += 24;   // 6 packed fma over 2 children
         // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
         // the 4-body tree's inner-child refs are byte offsets (node * 80,
         // written by rt_scene_upload): no multiply per step
@@ -803,6 +775,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         g3 = n3;
       }
     }
+    if constexpr (STATS && !is_bvh_scan(SCAN)) st_fl += 16ull * static_cast<uint64_t>(n);   // oc 3, h 5, c 6, disc 2
     if constexpr (STATS && !is_bvh_scan(SCAN)) {
       const uint64_t ex = __builtin_amdgcn_read_exec();
       if (lane == __ffsll(static_cast<long long>(ex)) - 1) st_sph += static_cast<uint64_t>(n);
@@ -817,6 +790,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     if (best < 0) {
       // sky (raytracing.clj:55-58)
+      if constexpr (STATS) st_fl += 12;
       const float sa = 0.5f * (uy + 1.0f);
       const float om = 1.0f - sa;
       cr = tr * fmaf(sa, 0.5f, om);
@@ -832,6 +806,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float hy = fmaf(uy, best_t, oy);
       const float hz = fmaf(uz, best_t, oz);
       // outward normal (p - C) / r, as (p - C) * (1/r) with 1/r from the table
+      if constexpr (STATS) st_fl += 17;   // p, n, front
       float nx = (hx - sp.x) * sp.w, ny = (hy - sp.y) * sp.w, nz = (hz - sp.z) * sp.w;
       const bool front = fmaf(dz, nz, fmaf(dy, ny, dx * nx)) < 0.0f;
       if (!front) {
@@ -850,7 +825,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         // the segment for these lanes): a wave loops the rejection sampler
         // once for both kinds
         float qx, qy, qz;
-        random_unit<STATS>(st, qx, qy, qz, &st_ball);
+        random_unit<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
+        if constexpr (STATS) st_fl += kind == RT_LAMBERTIAN ? 6 : 26;
         if (kind == RT_LAMBERTIAN) {
           // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
           float sx = qx + nx, sy = qy + ny, sz = qz + nz;
@@ -887,12 +863,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       } else {
         // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
         const float ri = front ? m.x : m.w;   // 1/eta (host-divided) : eta
+        if constexpr (STATS) st_fl += 9;
         const float un = fmaf(uz, nz, fmaf(uy, ny, ux * nx));
         const float cosv = fminf(-un, 1.0f);
         const float sinv = sqrt_rn(fmaf(-cosv, cosv, 1.0f));
         bool refl = !(ri * sinv <= 1.0f);
         if (!refl && !a.realm) {   // (realm: no Schlick term, no draw; realm/raytracing.clj:158-177)
           const float xi = rng_uniform(st);  // drawn only when refraction is possible
+          if constexpr (STATS) st_fl += 11;
           float r0 = (1.0f - ri) / (1.0f + ri);
           r0 = r0 * r0;
           const float x1 = 1.0f - cosv;
@@ -900,6 +878,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           const float x5 = x2 * x2 * x1;
           refl = fmaf(1.0f - r0, x5, r0) > xi;
         }
+        if constexpr (STATS) st_fl += refl ? 7 : 22;
         if (refl) {
           const float k2 = 2.0f * un;
           dx = fmaf(-nx, k2, ux);
@@ -922,139 +901,46 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       st_c_shade += t - st_ts;
       st_ts = t;
     }
-    if (POOL) {
-      if (done) {
-        float* d = scr + (q * a.pool_chunk + (k - c0)) * 3;   // [pixel][sample][rgb]
-        d[0] = cr;
-        d[1] = cg;
-        d[2] = cb;
-      }
-      const uint64_t m = __ballot(done);
-      if constexpr (WGP) {   // one LDS atomic per wave event: the next popc(m) indices
-        if (m) {
-          const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
-          int old = 0;
-          if (lane == leader) old = atomicAdd(&s_pool_next, static_cast<int>(__popcll(m)));
-          base = __builtin_amdgcn_readlane(old, leader);
-        }
-      }
-      if (done) {
-        j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
-        fresh = true;
-        if (j >= pool) active = false;
-      }
-      if constexpr (!WGP) base += static_cast<int>(__popcll(m));
-    } else if (done) {
-      accr += cr;
-      accg += cg;
-      accb += cb;
+    if (done) {   // the sample's colour into its pixel's fixed-point sum (order-free)
+      if constexpr (STATS) st_fl += 3;
+      unsigned long long* acc = &s_acc[q * 3];
+      __hip_atomic_fetch_add(acc + 0, static_cast<unsigned long long>(fix24(cr)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(acc + 1, static_cast<unsigned long long>(fix24(cg)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(acc + 2, static_cast<unsigned long long>(fix24(cb)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // refill: one LDS atomic per wave event hands out the next popc(m) indices
+    const uint64_t m = __ballot(done);
+    if (m) {
+      const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
+      int old = 0;
+      if (lane == leader) old = atomicAdd(&s_pool_next, static_cast<int>(__popcll(m)));
+      base = __builtin_amdgcn_readlane(old, leader);
+    }
+    if (done) {
+      j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
       fresh = true;
-      if (++k == k_next || k >= k_end) {
-        // a stripe is complete (the contract's sequential stripe sum)
-        if constexpr (LPP == 1) {
-          totr += accr;
-          totg += accg;
-          totb += accb;
-          accr = accg = accb = 0.0f;
-        } else if constexpr (LPP == 2) {
-          if (stripe == grp * SPL) {
-            s0r = accr;
-            s0g = accg;
-            s0b = accb;
-            accr = accg = accb = 0.0f;
-          }
-        }
-        ++stripe;
-        k_next = stripe_begin(stripe + 1, a.spp, P);
-      }
-      if (k >= k_end) active = false;
+      if (j >= pool) active = false;
     }
     if constexpr (STATS) st_c_acc += stamp() - st_ts;
   }
-  if constexpr (POOL) {
-    // the round's samples, in sample order, into lane (pixel pl, stripe
-    // grp)'s stripe sum (the wave's own stores: a workgroup-scope fence
-    // orders them); between rounds (launches) the sums wait in scratch
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if constexpr (WGP) __syncthreads();   // the other waves' samples too
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    float* const sums = scr + PPX * 3 * a.pool_chunk + (WGP ? static_cast<int>(threadIdx.x) : lane) * 6;
-    if (fp < npx && pool_work) {
-      if (c0 > 0) {
-        accr = sums[0];
-        accg = sums[1];
-        accb = sums[2];
-        totr = sums[3];
-        totg = sums[4];
-        totb = sums[5];
-      }
-      // LPP 4 shape: lane group grp's stripe; LPP 1 shape: every stripe, the
-      // completed ones into the running total
-      for (int sp = (LPPE == 4 ? grp : 0); sp < (LPPE == 4 ? grp + 1 : P); ++sp) {
-        const int b = stripe_begin(sp, a.spp, P), e = stripe_begin(sp + 1, a.spp, P);
-        const int sb = max(b, c0), se = min(e, c0 + cn);
-        for (int s = sb; s < se; ++s) {
-          const float* d = scr + (fp * a.pool_chunk + (s - c0)) * 3;
-          accr += d[0];
-          accg += d[1];
-          accb += d[2];
-        }
-        if (LPPE == 1 && e > c0 && e <= c0 + cn) {   // stripe sp completes in this round
-          totr += accr;
-          totg += accg;
-          totb += accb;
-          accr = accg = accb = 0.0f;
-        }
-      }
-      if (c0 + cn < a.spp) {   // more rounds follow: keep the sums, no output yet
-        sums[0] = accr;
-        sums[1] = accg;
-        sums[2] = accb;
-        sums[3] = totr;
-        sums[4] = totg;
-        sums[5] = totb;
-      }
-    }
-    px = qx0 + (vw > 0 ? fp % vw : 0);   // the fold lane's own pixel again
-    ro = qy0 + (vw > 0 ? fp / vw : 0);
-  }
 
-  // ---- per-pixel total ((s0 + s1) + s2) + s3, / spp (raytracing.clj:155) ----
-  float outr, outg, outb;
-  if constexpr (LPPE == 1) {
-    outr = totr;
-    outg = totg;
-    outb = totb;
-  } else if constexpr (LPPE == 2) {
-    // group 0 holds s0 (s0*) and s1 (acc*); group 1 holds s2 (s0*) and s3 (acc*)
-    const float s2r = __shfl(s0r, pl + PX), s2g = __shfl(s0g, pl + PX), s2b = __shfl(s0b, pl + PX);
-    const float s3r = __shfl(accr, pl + PX), s3g = __shfl(accg, pl + PX), s3b = __shfl(accb, pl + PX);
-    outr = ((s0r + accr) + s2r) + s3r;
-    outg = ((s0g + accg) + s2g) + s3g;
-    outb = ((s0b + accb) + s2b) + s3b;
-  } else {
-    // group g holds stripe g in acc*
-    const float s1r = __shfl(accr, pl + PX), s1g = __shfl(accg, pl + PX), s1b = __shfl(accb, pl + PX);
-    const float s2r = __shfl(accr, pl + 2 * PX), s2g = __shfl(accg, pl + 2 * PX), s2b = __shfl(accb, pl + 2 * PX);
-    const float s3r = __shfl(accr, pl + 3 * PX), s3g = __shfl(accg, pl + 3 * PX), s3b = __shfl(accb, pl + 3 * PX);
-    outr = ((accr + s1r) + s2r) + s3r;
-    outg = ((accg + s1g) + s2g) + s3g;
-    outb = ((accb + s1b) + s2b) + s3b;
-  }
-  if (in_image && grp == 0 && (!POOL || a.pool_c0 + a.pool_chunk >= a.spp)) {
+  // ---- per-pixel mean (compute-pixel's accum / spp, raytracing.clj:155) ----
+  // thread t < 3 * npx writes channel t % 3 of pool pixel t / 3: a tile row's
+  // 8 pixels are 24 consecutive floats
+  __syncthreads();
+  const int t = static_cast<int>(threadIdx.x);
+  if (t < npx * 3) {
+    const int fp = t / 3, ch = t - 3 * fp;
+    const int qy = vw == 1 ? fp : static_cast<int>(__umulhi(static_cast<uint32_t>(fp), mag_vw));
+    const int px = qx0 + (fp - qy * vw), ro = qy0 + qy;
+    const float tot = static_cast<float>(s_acc[t]) * 0x1p-24f;   // RN(float(sum)), exact scale
     const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
-    float* o = a.out + (static_cast<size_t>(ro) * a.width + px) * 3;
-    if (a.realm) {
-      const float sc = 1.0f / inv;   // pixel-scale (realm/raytracing.clj:25, :276)
-      o[0] = outr * sc;
-      o[1] = outg * sc;
-      o[2] = outb * sc;
-    } else {
-      o[0] = outr / inv;   // (vec3a/divide! accum samples-per-px) (:155)
-      o[1] = outg / inv;
-      o[2] = outb / inv;
-    }
+    // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
+    a.out[(static_cast<size_t>(ro) * a.width + px) * 3 + ch] = a.realm ? tot * (1.0f / inv) : tot / inv;
   }
 
   if (a.tile_cost && lane == 0) {   // the adaptive schedule's measurement
@@ -1079,11 +965,24 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[14], static_cast<unsigned long long>(st_ball));
       atomicAdd(&a.dbg[15], static_cast<unsigned long long>(st_disk));
     }
+    if (a.dbg && st_fresh) {
+      atomicAdd(&a.dbg[16], static_cast<unsigned long long>(st_fresh));
+      atomicAdd(&a.dbg[17], static_cast<unsigned long long>(st_fresh_lanes));
+    }
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));
       atomicAdd(&a.dbg[4], static_cast<unsigned long long>(st_blk_lanes));
     }
     if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+    {   // executed flops: a wave sum, one atomic
+      uint64_t f = st_fl;
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t lo = __shfl_xor(static_cast<uint32_t>(f), off);
+        const uint32_t hi = __shfl_xor(static_cast<uint32_t>(f >> 32), off);
+        f += (static_cast<uint64_t>(hi) << 32) | lo;
+      }
+      if (a.dbg && lane == 0) atomicAdd(&a.dbg[18], static_cast<unsigned long long>(f));
+    }
     // clock split: the lane active longest saw every iteration (max over lanes)
     const uint64_t c0 = wave_max_u64(st_c_cam), c1 = wave_max_u64(st_c_scan);
     const uint64_t c2 = wave_max_u64(st_c_shade), c3 = wave_max_u64(st_c_acc);
@@ -1104,18 +1003,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
   }
   if (a.counters) {
-    // one 64-bit atomic per wave: segments and samples of its 64 lanes
+    // one 64-bit atomic per wave: the segments of its 64 lanes; the samples
+    // once per workgroup
     uint32_t v = segs;
-    uint32_t smp = (in_image && grp == 0 && a.max_depth > 0 && a.spp > 0) ? static_cast<uint32_t>(a.spp) : 0u;
-    if (POOL && a.pool_c0 + a.pool_chunk < a.spp) smp = 0;   // counted by the last round
-    for (int off = 32; off > 0; off >>= 1) {
-      v += __shfl_xor(v, off);
-      smp += __shfl_xor(smp, off);
-    }
-    if (lane == 0) {
-      atomicAdd(&a.counters[0], static_cast<unsigned long long>(v));
-      atomicAdd(&a.counters[1], static_cast<unsigned long long>(smp));
-    }
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0 && v) atomicAdd(&a.counters[0], static_cast<unsigned long long>(v));
+    if (threadIdx.x == 0 && pool) atomicAdd(&a.counters[1], static_cast<unsigned long long>(pool));
   }
 }
 
@@ -1148,117 +1041,94 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
 }
 
 // ------------------------------------------------------------- host ------
-// Kernel variants (rt_set_variant):
-//   1 LDS table, simple scan        2 scalar-cache table, simple scan
-//   3 = 1 + stats                   4 LDS table, grouped scan (prefetch)
-//   5 scalar, grouped scan          6 = 4 + stats        7 = 5 + stats
-//   8 LDS table, packed pairs      9 scalar, packed pairs   10 = 9 + stats
-//  11 BVH in LDS                  12 BVH in global memory   13 = 11 + stats
-//  14 BVH in LDS, speculative while-while traversal          15 = 14 + stats
-//  16 BVH in LDS, 4-body leaves (two pairs)                  17 = 16 + stats
-//  18 BVH in LDS, 8-body leaves (four pairs)                 19 = 18 + stats
-//     (BVH variants fall back to 5 when the tree does not fit / is too deep)
-//   0 = default (16, or 18 when the 4-body tree's LDS image is large)
-// Lanes per pixel (rt_set_lanes_per_pixel): 1, 2, 4 = fixed sample stripes
-// per lane; -1 / -2 = the sample pool with 4 x 4 / 8 x 8 pixels per wave, -3 =
-// one pool of 8 x 8 pixels per workgroup (BVH variants 11, 13, 16-19); 0 =
-// automatic (-3 where the variant has it, else enough waves to keep the chip
-// full to the end).
+// Kernel variants (rt_set_variant).  The product library carries the default
+// traversal and its fallbacks:
+//   16 BVH in LDS, 4-body leaves (two pairs)      18 BVH in LDS, 8-body leaves
+//   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
+//    5 linear scan, grouped, table through the scalar cache: a tree too deep
+//    0 = default (16, or 18 when the 4-body tree's LDS image is large)
+// The diagnostic build (-DRTCLJ_DIAG, lib/librtclj_diag.so) adds the A/B and
+// statistics variants:
+//    1 LDS table, simple scan         2 scalar-cache table, simple scan
+//    3 = 1 + stats                    4 LDS table, grouped scan (north_star's LDS-staged scan)
+//    6 = 4 + stats                    7 = 5 + stats
+//    8 LDS table, packed pairs        9 scalar, packed pairs   10 = 9 + stats
+//   11 BVH in LDS, 2-body leaves     13 = 11 + stats
+//   14 11 with a speculative while-while traversal           15 = 14 + stats
+//   17 = 16 + stats                  19 = 18 + stats
+// Every variant renders the same bits.
 struct Variant {
-  const void* fn[6];   // LPP 1, 2, 4, sample pool 4 x 4 (LPP -1), 8 x 8 (-2), workgroup 8 x 8 (-3)
+  const void* fn;
   bool lds;
   bool stats;
 };
 constexpr int kVariants = 20;
 // the tree a traversal variant walks: 0 = 2-body leaves, 1 = 4, 2 = 8
 static int variant_tree(int v) { return v >= 18 ? 2 : v >= 16 ? 1 : 0; }
-#define RT_K(SRC, SCAN, LPP, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, LPP, ST>)
+#define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
 static const Variant& variant_table(int v) {
+  static const Variant none{nullptr, false, false};
   static const Variant t[kVariants] = {
-      {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false), RT_K(SRC_LDS, SCAN_BVH, -3, false)}, true, false},
-      {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, false), nullptr, nullptr}, true, false},
-      {{RT_K(SRC_SCALAR, SCAN_SIMPLE, 1, false), nullptr, nullptr}, false, false},
-      {{RT_K(SRC_LDS, SCAN_SIMPLE, 1, true), nullptr, nullptr}, true, true},
-      {{RT_K(SRC_LDS, SCAN_GROUP4, 1, false), RT_K(SRC_LDS, SCAN_GROUP4, 2, false),
-        RT_K(SRC_LDS, SCAN_GROUP4, 4, false)}, true, false},
-      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, false), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, false),
-        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, false)}, false, false},
-      {{RT_K(SRC_LDS, SCAN_GROUP4, 1, true), RT_K(SRC_LDS, SCAN_GROUP4, 2, true),
-        RT_K(SRC_LDS, SCAN_GROUP4, 4, true)}, true, true},
-      {{RT_K(SRC_SCALAR, SCAN_GROUP4, 1, true), RT_K(SRC_SCALAR, SCAN_GROUP4, 2, true),
-        RT_K(SRC_SCALAR, SCAN_GROUP4, 4, true)}, false, true},
-      {{RT_K(SRC_LDS, SCAN_PK4, 1, false), RT_K(SRC_LDS, SCAN_PK4, 2, false),
-        RT_K(SRC_LDS, SCAN_PK4, 4, false)}, true, false},
-      {{RT_K(SRC_SCALAR, SCAN_PK4, 1, false), RT_K(SRC_SCALAR, SCAN_PK4, 2, false),
-        RT_K(SRC_SCALAR, SCAN_PK4, 4, false)}, false, false},
-      {{RT_K(SRC_SCALAR, SCAN_PK4, 1, true), RT_K(SRC_SCALAR, SCAN_PK4, 2, true),
-        RT_K(SRC_SCALAR, SCAN_PK4, 4, true)}, false, true},
-      {{RT_K(SRC_LDS, SCAN_BVH, 1, false), RT_K(SRC_LDS, SCAN_BVH, 2, false),
-        RT_K(SRC_LDS, SCAN_BVH, 4, false), RT_K(SRC_LDS, SCAN_BVH, -1, false), RT_K(SRC_LDS, SCAN_BVH, -2, false), RT_K(SRC_LDS, SCAN_BVH, -3, false)}, true, false},
-      {{RT_K(SRC_SCALAR, SCAN_BVH, 1, false), RT_K(SRC_SCALAR, SCAN_BVH, 2, false),
-        RT_K(SRC_SCALAR, SCAN_BVH, 4, false)}, false, false},
-      {{RT_K(SRC_LDS, SCAN_BVH, 1, true), RT_K(SRC_LDS, SCAN_BVH, 2, true),
-        RT_K(SRC_LDS, SCAN_BVH, 4, true), RT_K(SRC_LDS, SCAN_BVH, -1, true), RT_K(SRC_LDS, SCAN_BVH, -2, true), RT_K(SRC_LDS, SCAN_BVH, -3, true)}, true, true},
-      {{RT_K(SRC_LDS, SCAN_BVHWW, 1, false), RT_K(SRC_LDS, SCAN_BVHWW, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHWW, 4, false)}, true, false},
-      {{RT_K(SRC_LDS, SCAN_BVHWW, 1, true), RT_K(SRC_LDS, SCAN_BVHWW, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHWW, 4, true)}, true, true},
-      {{RT_K(SRC_LDS, SCAN_BVHQ, 1, false), RT_K(SRC_LDS, SCAN_BVHQ, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, false), RT_K(SRC_LDS, SCAN_BVHQ, -1, false), RT_K(SRC_LDS, SCAN_BVHQ, -2, false), RT_K(SRC_LDS, SCAN_BVHQ, -3, false)}, true, false},
-      {{RT_K(SRC_LDS, SCAN_BVHQ, 1, true), RT_K(SRC_LDS, SCAN_BVHQ, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHQ, 4, true), RT_K(SRC_LDS, SCAN_BVHQ, -1, true), RT_K(SRC_LDS, SCAN_BVHQ, -2, true), RT_K(SRC_LDS, SCAN_BVHQ, -3, true)}, true, true},
-      {{RT_K(SRC_LDS, SCAN_BVHO, 1, false), RT_K(SRC_LDS, SCAN_BVHO, 2, false),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, false), RT_K(SRC_LDS, SCAN_BVHO, -1, false), RT_K(SRC_LDS, SCAN_BVHO, -2, false), RT_K(SRC_LDS, SCAN_BVHO, -3, false)}, true, false},
-      {{RT_K(SRC_LDS, SCAN_BVHO, 1, true), RT_K(SRC_LDS, SCAN_BVHO, 2, true),
-        RT_K(SRC_LDS, SCAN_BVHO, 4, true), RT_K(SRC_LDS, SCAN_BVHO, -1, true), RT_K(SRC_LDS, SCAN_BVHO, -2, true), RT_K(SRC_LDS, SCAN_BVHO, -3, true)}, true, true},
+      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false},          // 0: placeholder (resolved per scene)
+#ifdef RTCLJ_DIAG
+      {RT_K(SRC_LDS, SCAN_SIMPLE, false), true, false},        // 1
+      {RT_K(SRC_SCALAR, SCAN_SIMPLE, false), false, false},    // 2
+      {RT_K(SRC_LDS, SCAN_SIMPLE, true), true, true},          // 3
+      {RT_K(SRC_LDS, SCAN_GROUP4, false), true, false},        // 4
+#else
+      none, none, none, none,
+#endif
+      {RT_K(SRC_SCALAR, SCAN_GROUP4, false), false, false},    // 5
+#ifdef RTCLJ_DIAG
+      {RT_K(SRC_LDS, SCAN_GROUP4, true), true, true},          // 6
+      {RT_K(SRC_SCALAR, SCAN_GROUP4, true), false, true},      // 7
+      {RT_K(SRC_LDS, SCAN_PK4, false), true, false},           // 8
+      {RT_K(SRC_SCALAR, SCAN_PK4, false), false, false},       // 9
+      {RT_K(SRC_SCALAR, SCAN_PK4, true), false, true},         // 10
+      {RT_K(SRC_LDS, SCAN_BVH, false), true, false},           // 11
+#else
+      none, none, none, none, none, none,
+#endif
+      {RT_K(SRC_SCALAR, SCAN_BVH, false), false, false},       // 12
+#ifdef RTCLJ_DIAG
+      {RT_K(SRC_LDS, SCAN_BVH, true), true, true},             // 13
+      {RT_K(SRC_LDS, SCAN_BVHWW, false), true, false},         // 14
+      {RT_K(SRC_LDS, SCAN_BVHWW, true), true, true},           // 15
+#else
+      none, none, none,
+#endif
+      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false},          // 16
+#ifdef RTCLJ_DIAG
+      {RT_K(SRC_LDS, SCAN_BVHQ, true), true, true},            // 17
+#else
+      none,
+#endif
+      {RT_K(SRC_LDS, SCAN_BVHO, false), true, false},          // 18
+#ifdef RTCLJ_DIAG
+      {RT_K(SRC_LDS, SCAN_BVHO, true), true, true},            // 19
+#else
+      none,
+#endif
   };
-  return t[(v >= 0 && v < kVariants) ? v : 0];
+  return (v >= 0 && v < kVariants) ? t[v] : none;
 }
 #undef RT_K
-static int g_lpp = 0;  // 0 = automatic, -1 / -2 = sample pool 4 x 4 / 8 x 8
-// sample-pool scratch per launch (beyond it: more rounds).  A workgroup's pool
-// should hold ~100+ samples per pixel: shorter pools end more often, and every
-// end idles lanes until the pool's last path is done (C2 at 500 spp: 20-sample
-// rounds 8150 Msamples/s, 172-sample rounds 11380).  Default: 1/8 of the
-// device's memory (36 GB on an MI355X), at most half of what is free, at
-// least 2 GB; RTCLJ_POOL_BYTES overrides it (tests: many rounds, small frame).
-static size_t pool_bytes_env() {
-  const char* e = std::getenv("RTCLJ_POOL_BYTES");
-  const long long v = e ? std::atoll(e) : 0;
-  return v > 0 ? static_cast<size_t>(v) : 0;
-}
-static size_t pool_bytes_default() {
-  size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return size_t(2) << 30;
-  return std::max(size_t(2) << 30, std::min(total_b / 8, free_b / 2));
-}
-
-// Lanes per pixel: more lanes per pixel = more, shorter waves (the frame's
-// last waves then drain quickly); 1 lane keeps the SIMD fuller per wave.
-static int fn_slot(int lpp) { return lpp == -1 ? 3 : lpp == -2 ? 4 : lpp == -3 ? 5 : lpp == 1 ? 0 : lpp == 2 ? 1 : 2; }
-static int choose_lpp(int width, int rows, int spp, const Variant& v) {
-  const auto has = [&](int lpp) { return v.fn[fn_slot(lpp)] != nullptr && (lpp < 0 || lpp == 1 || spp >= 4); };
-  if (g_lpp != 0 && has(g_lpp)) return g_lpp;
-  if (has(-3)) return -3;   // automatic: the workgroup sample pool where the variant has it
-  if (!v.fn[2] || spp < 4) return v.fn[0] ? 1 : -3;
-  const long long target = 48 * 1024;  // ~6 x the waves an MI355X keeps resident
-  const long long w1 = 4LL * ((width + 15) / 16) * ((rows + 15) / 16);
-  const long long w2 = 4LL * ((width + 15) / 16) * ((rows + 7) / 8);
-  if (w1 >= target && v.fn[0]) return 1;
-  if (w2 >= target && v.fn[1]) return 2;
-  return 4;
-}
-static int g_variant = 0;
-// tile schedule (rt_set_schedule): 0 = adaptive longest-first, 1 = dispatch order
-static int g_schedule = 0;
+// selectors (rt_set_variant / rt_set_schedule): atomics, read once per launch
+static std::atomic<int> g_variant{0};
+// tile schedule: 0 = adaptive longest-first, 1 = dispatch order
+static std::atomic<int> g_schedule{0};
 // BVH build: surface-area splits (default) or median splits (RTCLJ_BVH=median, for A/B)
 static const bool g_bvh_sah = [] {
   const char* e = std::getenv("RTCLJ_BVH");
   return !(e && std::strcmp(e, "median") == 0);
 }();
-static unsigned long long* g_dbg = nullptr;   // device u64[8] for variant 3 (per process, device 0)
-static unsigned long long* g_dbgw = nullptr;  // device u64[4 * 65536] wave timeline for variant 3
+// stats builds: per device, u64[kDbg] event counters and the u64[4 * 65536]
+// wave timeline, allocated on that device at its first stats launch
+constexpr int kDbg = 32;
+constexpr int kDbgDevices = 64;
+static std::mutex g_dbg_mu;
+static unsigned long long* g_dbg[kDbgDevices] = {};
+static unsigned long long* g_dbgw[kDbgDevices] = {};
 
 }  // namespace rtclj
 
@@ -1273,23 +1143,21 @@ struct DTree {
 
 // Adaptive tile schedule (rt_launch): per stream, the per-tile durations of
 // the stream's last launch and the longest-first order derived from them, for
-// the launch shape `key` (frame rows, tiling, lanes per pixel, grid).  The
-// order is a prediction: camera, spp, seed, flags and the kernel variant may
-// change between launches of one shape (progressive passes, animation, A/B)
-// and it stays a good one, and it never affects the result.  A launch of another shape re-keys the
-// entry (and runs in dispatch order once).  Entries are per stream so that nothing a
-// stream's kernels read is written from another stream; a dscene serves up to
-// kSchedStreams streams this way, launches on further streams run unscheduled.
+// the launch shape `key` (frame rows, tiling, grid).  The order is a
+// prediction: camera, spp, seed, flags and the kernel variant may change
+// between launches of one shape (progressive passes, animation, A/B) and it
+// stays a good one, and it never affects the result.  A launch of another
+// shape re-keys the entry (and runs in dispatch order once).  Entries are per
+// stream so that nothing a stream's kernels read is written from another
+// stream; a dscene serves up to kSchedStreams streams this way, launches on
+// further streams run unscheduled.
 struct ScheduleKey {
-  int width, rows, row_begin, row_tile, tile_first, tile_step, lpp, gx, gy;
+  int width, rows, row_begin, row_tile, tile_first, tile_step, gx, gy;
 };
 struct Schedule {
   hipStream_t stream = nullptr;
   unsigned* cost = nullptr;
   int* order = nullptr;
-  float* scratch = nullptr;   // the sample pool's per-wave sample colours
-  size_t scratch_bytes = 0;
-  size_t pool_budget = 0;     // default scratch budget (pool_bytes_default(), at the stream's first pool launch)
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
@@ -1303,7 +1171,6 @@ struct ScheduleSet {
     for (int k = 0; k < used; ++k) {
       if (s[k].cost) (void)hipFree(s[k].cost);
       if (s[k].order) (void)hipFree(s[k].order);
-      if (s[k].scratch) (void)hipFree(s[k].scratch);
     }
     used = 0;
   }
@@ -1334,21 +1201,17 @@ static int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 extern "C" int rt_set_variant(int v) {
-  const int old = g_variant;
-  if (v >= 0 && v < kVariants) g_variant = v;
-  return old;
+  clear_error();
+  if (v != 0 && !variant_table(v).fn)
+    return set_error(RT_E_ARG, "rt_set_variant: variant " + std::to_string(v) +
+                                   " is not in this build (diagnostic variants: lib/librtclj_diag.so)");
+  return g_variant.exchange(v);
 }
 
 extern "C" int rt_set_schedule(int mode) {
-  const int old = g_schedule;
-  if (mode == 0 || mode == 1) g_schedule = mode;
-  return old;
-}
-
-extern "C" int rt_set_lanes_per_pixel(int lpp) {
-  const int old = g_lpp;
-  if (lpp >= -3 && lpp <= 4 && lpp != 3) g_lpp = lpp;
-  return old;
+  clear_error();
+  if (mode != 0 && mode != 1) return set_error(RT_E_ARG, "rt_set_schedule: mode must be 0 or 1");
+  return g_schedule.exchange(mode);
 }
 
 extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
@@ -1475,6 +1338,10 @@ static size_t stack_of(const DTree& t, int tree) {
   return static_cast<size_t>(t.depth + 2) * 256 * (tree == 2 ? 1 : 2);
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
+// LDS a CU can give each of 5 workgroups (160 KB / 5), less the kernel's
+// static LDS (pool counter + the 64 pixels' colour sums)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;
+constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
 static int resolve_variant(const rt_dscene& ds, int vsel) {
@@ -1482,7 +1349,7 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
   // the 5 workgroups the registers allow (160 KB / 5) and the 8-body-leaf
   // tree's is smaller (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
   if (vsel == 0)
-    vsel = (lds_of(ds.tree[1], 1) > 32 * 1024 && ds.tree[2].n_nodes <= 256 &&
+    vsel = (lds_of(ds.tree[1], 1) > kLds5 && ds.tree[2].n_nodes <= 256 &&
             lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
   if ((vsel == 18 || vsel == 19) && ds.tree[2].n_nodes > 256) vsel -= 2;   // u8 stack: 256 nodes at most
   if ((vsel == 16 || vsel == 17) && ds.tree[1].n_nodes * 80 > 65535) vsel = 12;   // u16 stack of byte offsets
@@ -1495,7 +1362,17 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
   return vsel;
 }
 
-extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_variant(*ds, g_variant) : -1; }
+extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_variant(*ds, g_variant.load()) : -1; }
+
+// dynamic LDS of a launch of variant vsel on ds
+static size_t launch_lds(const rt_dscene& ds, int vsel) {
+  const Variant& v = variant_table(vsel);
+  if (vsel >= 11) {
+    const DTree& tr = ds.tree[variant_tree(vsel)];
+    return v.lds ? lds_of(tr, variant_tree(vsel)) : stack_of(tr, variant_tree(vsel));
+  }
+  return v.lds ? static_cast<size_t>(ds.n_pad) * sizeof(float4) : 0;
+}
 
 // Occupancy of the launch rt_launch would make for (ds, p): the HIP occupancy
 // query on the kernel and dynamic LDS it would use (diagnostic, bench.py).
@@ -1505,14 +1382,10 @@ extern "C" int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int*
   const int rows = rows_out(*p);
   if (rows <= 0 || p->width <= 0) return set_error(RT_E_ARG, "rt_launch_occupancy: empty frame");
   HIP_TRY(hipSetDevice(ds->device));
-  const int vsel = resolve_variant(*ds, g_variant);
-  const DTree& tr = ds->tree[variant_tree(vsel)];
-  const Variant& v = variant_table(vsel);
-  const int lpp = choose_lpp(p->width, rows, p->spp, v);
-  const void* fn = v.fn[fn_slot(lpp)];
-  if (!fn) return set_error(RT_E_ARG, "rt_launch_occupancy: no launch shape");
-  const size_t lds = vsel >= 11 ? (v.lds ? lds_of(tr, variant_tree(vsel)) : stack_of(tr, variant_tree(vsel)))
-                                : (v.lds ? static_cast<size_t>(ds->n_pad) * sizeof(float4) : 0);
+  const int vsel = resolve_variant(*ds, g_variant.load());
+  const void* fn = variant_table(vsel).fn;
+  if (!fn) return set_error(RT_E_ARG, "rt_launch_occupancy: no kernel for variant " + std::to_string(vsel));
+  const size_t lds = launch_lds(*ds, vsel);
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   int blocks = 0;
@@ -1522,7 +1395,21 @@ extern "C" int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int*
   out4[0] = blocks;               // 256-thread workgroups per CU
   out4[1] = fa.numRegs;           // VGPRs per lane
   out4[2] = static_cast<int>(lds + fa.sharedSizeBytes);   // LDS bytes per workgroup
-  out4[3] = lpp;
+  out4[3] = vsel;
+  return RT_OK;
+}
+
+static int dbg_buffers(int device, unsigned long long** dbg, unsigned long long** dbgw) {
+  if (device < 0 || device >= kDbgDevices) return set_error(RT_E_ARG, "stats launch: device index too large");
+  std::lock_guard<std::mutex> lk(g_dbg_mu);
+  if (!g_dbg[device]) {
+    HIP_TRY(hipMalloc(&g_dbg[device], kDbg * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(g_dbg[device], 0, kDbg * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&g_dbgw[device], 4 * 65536 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * 65536 * sizeof(unsigned long long)));
+  }
+  *dbg = g_dbg[device];
+  *dbgw = g_dbgw[device];
   return RT_OK;
 }
 
@@ -1530,7 +1417,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();
   if (!ds || !c || !p || !d_out) return set_error(RT_E_ARG, "rt_launch: NULL argument");
-  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || (p->flags & ~RT_FLAG_REALM) != 0)
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP || (p->flags & ~RT_FLAG_REALM) != 0)
     return set_error(RT_E_ARG, "rt_launch: bad width/height/spp/flags");
   const int rows = rows_out(*p);
   if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
@@ -1560,16 +1447,16 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.spp = p->spp;
   a.sample_begin = p->sample_begin;
   a.max_depth = p->max_depth;
+  // j / spp by multiply-high: exact for j < 64 * spp while 64 * spp^2 <= 2^32
+  a.spp_magic = (p->spp > 1 && p->spp <= 8191) ? static_cast<uint32_t>(0xffffffffu / static_cast<uint32_t>(p->spp)) + 1u : 0u;
   a.realm = (p->flags & RT_FLAG_REALM) ? 1 : 0;
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
-  const int vsel = resolve_variant(*ds, g_variant);
-  const DTree& tr = ds->tree[variant_tree(vsel)];
-  const size_t stack_bytes = stack_of(tr, variant_tree(vsel));
-  const size_t bvh_lds = lds_of(tr, variant_tree(vsel));
+  const int vsel = resolve_variant(*ds, g_variant.load());
   const Variant& v = variant_table(vsel);
-  const bool is_bvh = vsel >= 11;
+  if (!v.fn) return set_error(RT_E_ARG, "rt_launch: no kernel for variant " + std::to_string(vsel));
+  const DTree& tr = ds->tree[variant_tree(vsel)];
   a.bvh_blob = tr.blob;
   a.bvh_blob_f4 = tr.blob_f4;
   a.bvh_off_pairs = tr.off_pairs;
@@ -1580,12 +1467,21 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  int lpp = choose_lpp(p->width, rows, p->spp, v);
-  // per-stream state of this scene: the adaptive schedule's record and the
-  // sample pool's scratch (both only ever used by this stream's kernels)
+  const dim3 grid((p->width + kTile - 1) / kTile, (rows + kTile - 1) / kTile);
+  const dim3 block(256);
+  const int n_tiles = static_cast<int>(grid.x * grid.y);
+  if (v.stats) {
+    const int rc = dbg_buffers(ds->device, &a.dbg, &a.dbgw);
+    if (rc != RT_OK) return rc;
+  }
+  const size_t lds = launch_lds(*ds, vsel);
+  if (lds > 64 * 1024)
+    HIP_TRY(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  // adaptive schedule: dispatch tiles longest first, by the durations the
+  // previous launch of this launch shape on this scene and stream measured
   Schedule* sch = nullptr;
   std::unique_lock<std::mutex> sched_lock;
-  if (g_schedule == 0 || lpp < 0) {
+  if (g_schedule.load() == 0) {
     ScheduleSet& set = ds->sched;
     sched_lock = std::unique_lock<std::mutex>(set.mu);
     for (int k = 0; k < set.used && !sch; ++k)
@@ -1594,65 +1490,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch = &set.s[set.used++];
       sch->stream = stream;
     }
-    if (!sch && lpp < 0) lpp = p->spp >= 4 && v.fn[2] ? 4 : 1;   // no slot for a pool: stripes (same bits)
   }
-  const int tw = (lpp == 4 || lpp == -1 || lpp == -3) ? 4 : 8, th = (lpp == 1 || lpp == -2) ? 8 : 4;   // wave tile
-  const dim3 grid((p->width + 2 * tw - 1) / (2 * tw), (rows + 2 * th - 1) / (2 * th));
-  const dim3 block(256);
-  const void* fn = v.fn[fn_slot(lpp)];
-  if (!fn) return set_error(RT_E_ARG, "rt_launch: kernel variant " + std::to_string(vsel) + " has no launch shape for this frame");
-  const int n_tiles = static_cast<int>(grid.x * grid.y);
-  if (v.stats) {
-    if (!g_dbg) {
-      HIP_TRY(hipMalloc(&g_dbg, 16 * sizeof(unsigned long long)));
-      HIP_TRY(hipMemset(g_dbg, 0, 16 * sizeof(unsigned long long)));
-      HIP_TRY(hipMalloc(&g_dbgw, 4 * 65536 * sizeof(unsigned long long)));
-      HIP_TRY(hipMemset(g_dbgw, 0, 4 * 65536 * sizeof(unsigned long long)));
-    }
-    a.dbg = g_dbg;
-    a.dbgw = g_dbgw;
-  }
-  size_t lds = 0;
-  if (is_bvh) {
-    lds = v.lds ? bvh_lds : stack_bytes;
-    if (lds > 64 * 1024)
-      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-  } else if (v.lds) {
-    lds = static_cast<size_t>(ds->n_pad) * sizeof(float4);
-    if (lds > 64 * 1024)
-      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-  }
-  if (lpp < 0) {
-    // pool scratch: per wave 16 / 64 pixels x chunk samples x rgb, chunk = spp
-    // up to the scratch budget for the whole launch (more rounds beyond that), + the
-    // 64 lanes' sums between rounds (6 floats)
-    // RTCLJ_POOL_BYTES per launch; the device default once per scene and stream
-    size_t budget = pool_bytes_env();
-    if (budget == 0) {
-      if (sch->pool_budget == 0) sch->pool_budget = pool_bytes_default();
-      budget = sch->pool_budget;
-    }
-    const size_t waves = static_cast<size_t>(n_tiles) * 4;
-    const size_t per_sample = waves * (lpp == -2 ? 64 : 16) * 3 * sizeof(float);   // (-3: 64 per 4 waves)
-    const int chunk = static_cast<int>(std::max<size_t>(
-        1, std::min<size_t>({static_cast<size_t>(p->spp > 0 ? p->spp : 1), budget / per_sample, 16384})));
-    const size_t need = per_sample * chunk + waves * 64 * 6 * sizeof(float);
-    if (sch->scratch_bytes < need) {   // grow (this stream's kernels may still use the old one)
-      HIP_TRY(hipStreamSynchronize(stream));
-      if (sch->scratch) (void)hipFree(sch->scratch);
-      sch->scratch = nullptr;
-      sch->scratch_bytes = 0;
-      HIP_TRY(hipMalloc(&sch->scratch, need));
-      sch->scratch_bytes = need;
-    }
-    a.pool_scratch = sch->scratch;
-
-    a.pool_chunk = chunk;
-  }
-  // adaptive schedule: dispatch tiles longest first, by the durations the
-  // previous launch of this launch shape on this scene and stream measured
-  bool scheduled = false;
-  if (g_schedule == 0 && sch) {
+  if (sch) {
     ScheduleKey key{};
     key.width = a.width;
     key.rows = a.rows_out;
@@ -1660,7 +1499,6 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     key.row_tile = a.row_tile;
     key.tile_first = a.tile_first;
     key.tile_step = a.tile_step;
-    key.lpp = lpp;
     key.gx = static_cast<int>(grid.x);
     key.gy = static_cast<int>(grid.y);
     if (std::memcmp(&sch->key, &key, sizeof key) != 0) {
@@ -1682,18 +1520,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
     HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
-    scheduled = true;
   }
   void* args[] = {&a};
-  if (lpp < 0) {   // the sample pool: one launch per round of pool_chunk samples per pixel
-    for (a.pool_c0 = 0;; a.pool_c0 += a.pool_chunk) {
-      HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
-      if (a.pool_c0 + a.pool_chunk >= p->spp) break;
-    }
-  } else {
-    HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, stream));
-  }
-  if (scheduled) {
+  HIP_TRY(hipLaunchKernel(v.fn, grid, block, args, lds, stream));
+  if (sch) {
     // the next launch's order, stream-ordered after this kernel (no host sync)
     const unsigned* cost = sch->cost;
     int* order = sch->order;
@@ -1706,27 +1536,37 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   return RT_OK;
 }
 
-// Stats builds read-back: copies and clears the 16 debug counters.
-extern "C" int rt_debug_stats(uint64_t* out16) {
-  if (!out16) return set_error(RT_E_ARG, "rt_debug_stats: NULL");
-  if (!g_dbg) {
-    for (int i = 0; i < 16; ++i) out16[i] = 0;
-    return RT_OK;
+// Stats builds read-back: sums and clears the kDbg debug counters of every
+// device that ran a stats launch.
+extern "C" int rt_debug_stats(uint64_t* out32) {
+  clear_error();
+  if (!out32) return set_error(RT_E_ARG, "rt_debug_stats: NULL");
+  for (int i = 0; i < kDbg; ++i) out32[i] = 0;
+  std::lock_guard<std::mutex> lk(g_dbg_mu);
+  for (int d = 0; d < kDbgDevices; ++d) {
+    if (!g_dbg[d]) continue;
+    uint64_t v[kDbg];
+    HIP_TRY(hipSetDevice(d));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(v, g_dbg[d], sizeof v, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(g_dbg[d], 0, sizeof v));
+    for (int i = 0; i < kDbg; ++i) out32[i] += v[i];
   }
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out16, g_dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemset(g_dbg, 0, 16 * sizeof(uint64_t)));
   return RT_OK;
 }
 
-// Stats build (variant 3) wave timeline: up to n waves x {t_start, t_end,
+// Stats build wave timeline of `device`: up to n waves x {t_start, t_end,
 // hw_id, xcc_id} (s_memrealtime ticks, 100 MHz); cleared after the copy.
-extern "C" int rt_debug_waves(uint64_t* out, size_t n_waves) {
+extern "C" int rt_debug_waves(int device, uint64_t* out, size_t n_waves) {
+  clear_error();
   if (!out) return set_error(RT_E_ARG, "rt_debug_waves: NULL");
-  if (!g_dbgw) return 0;
+  if (device < 0 || device >= kDbgDevices) return set_error(RT_E_ARG, "rt_debug_waves: bad device");
+  std::lock_guard<std::mutex> lk(g_dbg_mu);
+  if (!g_dbgw[device]) return 0;
   if (n_waves > 65536) n_waves = 65536;
+  HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, g_dbgw, 4 * n_waves * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemset(g_dbgw, 0, 4 * 65536 * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpy(out, g_dbgw[device], 4 * n_waves * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * 65536 * sizeof(uint64_t)));
   return static_cast<int>(n_waves);
 }

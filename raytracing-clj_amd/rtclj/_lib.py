@@ -13,10 +13,13 @@ from pathlib import Path
 _PKG_ROOT = Path(__file__).resolve().parent.parent          # raytracing-clj_amd/
 # RTCLJ_LIBRARY: load another build of the same ABI (A/B of kernel builds)
 library_path = Path(os.environ["RTCLJ_LIBRARY"]) if os.environ.get("RTCLJ_LIBRARY") else _PKG_ROOT / "lib" / "librtclj.so"
+# the diagnostic build (A/B and statistics kernel variants; same ABI)
+diag_library_path = _PKG_ROOT / "lib" / "librtclj_diag.so"
 
 RT_OK, RT_E_ARG, RT_E_MATERIAL, RT_E_TOO_MANY, RT_E_HIP, RT_E_NODEV, RT_E_IO = 0, -1, -2, -3, -4, -5, -6
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC, RT_NONE = 0, 1, 2, 3
 RT_MAX_SPHERES = 8192
+RT_MAX_SPP = 1 << 24
 RT_FLAG_SHARDS_ON_DEVICE0 = 1
 RT_FLAG_REALM = 2
 
@@ -56,7 +59,11 @@ class rt_params(C.Structure):
 
 class rt_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("kernel_ms", C.c_double),
-                ("total_ms", C.c_double), ("n_devices", C.c_int)]
+                ("total_ms", C.c_double), ("n_devices", C.c_int), ("scene_cached", C.c_int),
+                ("upload_ms", C.c_double), ("gather_ms", C.c_double), ("kernel_ms_mean", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 # symbol -> (restype, argtypes); every function include/rt.h declares
@@ -73,6 +80,7 @@ SIGNATURES = {
                                  C.POINTER(C.c_float), C.c_int]),
     "rt_render": (C.c_int, [C.POINTER(rt_scene), C.POINTER(rt_camera), C.POINTER(rt_params),
                             C.POINTER(C.c_float), C.c_size_t, C.POINTER(rt_stats)]),
+    "rt_cache_clear": (C.c_int, []),
     "rt_scene_upload": (C.c_int, [C.c_int, C.POINTER(rt_scene), C.POINTER(C.c_void_p)]),
     "rt_scene_free": (C.c_int, [C.c_void_p]),
     "rt_launch": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_params), C.c_void_p,
@@ -80,21 +88,23 @@ SIGNATURES = {
     "rt_set_variant": (C.c_int, [C.c_int]),
     "rt_resolve_variant": (C.c_int, [C.c_void_p]),
     "rt_launch_occupancy": (C.c_int, [C.c_void_p, C.POINTER(rt_params), C.POINTER(C.c_int)]),
-    "rt_set_lanes_per_pixel": (C.c_int, [C.c_int]),
     "rt_set_schedule": (C.c_int, [C.c_int]),
     "rt_debug_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
-    "rt_debug_waves": (C.c_int, [C.POINTER(C.c_uint64), C.c_size_t]),
+    "rt_debug_waves": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_device_count": (C.c_int, []),
     "rt_last_error": (C.c_char_p, []),
     "rt_version": (C.c_char_p, []),
 }
 
 
-def _load() -> C.CDLL:
-    if not library_path.exists():
-        raise ImportError(f"{library_path} is missing: build it with `make -C {_PKG_ROOT}` "
+def load(path: Path) -> C.CDLL:
+    """Load a build of include/rt.h's ABI with every signature bound.  Local
+    binding (RTLD_LOCAL; the library exports only rt_* symbols): the product
+    and the diagnostic build can be loaded side by side."""
+    if not Path(path).exists():
+        raise ImportError(f"{path} is missing: build it with `make -C {_PKG_ROOT}` "
                           "(or __graft_entry__.build()); there is no CPU fallback")
-    dll = C.CDLL(str(library_path), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    dll = C.CDLL(str(path), mode=os.RTLD_NOW | os.RTLD_LOCAL)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(dll, name)
         fn.restype = res
@@ -102,7 +112,17 @@ def _load() -> C.CDLL:
     return dll
 
 
-lib = _load()
+lib = load(library_path)
+_diag = None
+
+
+def diag_lib() -> C.CDLL:
+    """The diagnostic build (lib/librtclj_diag.so: the A/B and statistics
+    kernel variants, rt_set_variant 1-19), loaded on first use."""
+    global _diag
+    if _diag is None:
+        _diag = load(diag_library_path)
+    return _diag
 
 
 def check(code: int) -> int:

@@ -122,11 +122,13 @@ def camera(image_width, image_h, vfov, look_from, look_at, vup, defocus_angle, f
 
 def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50, seed: int = 1,
            n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None,
-           flags: int = 0):
+           flags: int = 0, library=None):
     """compute-pixel for every pixel of rows [r0, r1) (default: all), on the GPU.
 
     Returns float32 (rows, width, 3) linear RGB, each pixel the mean of its spp
-    samples (raytracing.clj:155).  `scene` is a Scene or a list of bodies."""
+    samples (raytracing.clj:155).  `scene` is a Scene or a list of bodies.
+    `library`: another loaded build of the ABI (rtclj._lib.diag_lib())."""
+    dll = library if library is not None else lib
     if not isinstance(scene, Scene):
         scene = Scene.from_bodies(scene)
     r0, r1 = (0, height) if rows is None else rows
@@ -134,10 +136,11 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
                   seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
     out = np.empty((max(r1 - r0, 0), width, 3), np.float32)
     st = rt_stats()
-    check(lib.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st)))
+    code = dll.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st))
+    if code < 0:
+        raise RTError(code, dll.rt_last_error().decode(errors="replace"))
     if stats is not None:
-        stats.update(segments=st.segments, samples=st.samples, kernel_ms=st.kernel_ms, total_ms=st.total_ms,
-                     n_devices=st.n_devices)
+        stats.update(st.as_dict())
     return out
 
 

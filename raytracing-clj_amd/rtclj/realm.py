@@ -70,10 +70,10 @@ def camera(image_width: int, image_h: int):
 
 
 def render(scene, cam, width: int, height: int, spp: int = SAMPLES_PER_PX, max_depth: int = MAX_DEPTH,
-           seed: int = 1, n_devices: int = 0, rows=None, stats: dict | None = None, flags: int = 0):
+           seed: int = 1, n_devices: int = 0, rows=None, stats: dict | None = None, flags: int = 0, library=None):
     """The realm loop (realm/raytracing.clj:339-357) for every pixel, on the GPU."""
     return R.render(scene, cam, width, height, spp, max_depth, seed=seed, n_devices=n_devices, rows=rows,
-                    stats=stats, flags=flags | RT_FLAG_REALM)
+                    stats=stats, flags=flags | RT_FLAG_REALM, library=library)
 
 
 def main(out_path="scene-realm.ppm", seed: int = 1, n_devices: int = 0, png_path=None) -> np.ndarray:

@@ -23,13 +23,15 @@ def test_header_declares_the_expected_boundary():
         assert name in fns
 
 
-def test_library_exports_every_declared_symbol():
+@pytest.mark.parametrize("which", ["product", "diag"])
+def test_library_exports_every_declared_symbol(which):
     import rtclj
-    from rtclj._lib import SIGNATURES
-    dll = C.CDLL(str(rtclj.library_path))
+    from rtclj._lib import SIGNATURES, diag_library_path
+    dll = C.CDLL(str(rtclj.library_path if which == "product" else diag_library_path))
     for name in declared_functions():
         assert hasattr(dll, name), f"{name} declared in rt.h but not exported"
         assert name in SIGNATURES, f"{name} has no ctypes signature in rtclj._lib"
+    assert set(SIGNATURES) == set(declared_functions())
 
 
 def test_exports_are_unmangled_c():
@@ -40,6 +42,9 @@ def test_exports_are_unmangled_c():
         pytest.skip("nm unavailable")
     syms = set(re.findall(r"\b(rt_[a-z_0-9]+)\b", out.stdout))
     assert set(declared_functions()) <= syms
+    # -fvisibility=hidden: no C++ functions leak (kernel handles aside)
+    funcs = [ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln]
+    assert all(f.startswith("rt_") for f in funcs), [f for f in funcs if not f.startswith("rt_")]
 
 
 def test_struct_layouts_match_header():
@@ -47,7 +52,7 @@ def test_struct_layouts_match_header():
     assert C.sizeof(rt_camera) == 18 * 4 + 4
     assert C.sizeof(rt_scene) == 32
     assert rt_params.seed.offset == 24 and C.sizeof(rt_params) == 56
-    assert C.sizeof(rt_stats) == 40
+    assert C.sizeof(rt_stats) == 64 and rt_stats.upload_ms.offset == 40
 
 
 def test_no_gpu_here_fails_loudly():
@@ -84,6 +89,8 @@ def test_argument_errors():
     assert b"out_len" in lib.rt_last_error()
     p_flag = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=1, max_depth=5, flags=8)
     assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_flag), fp, out.size, None) == -1
+    p_spp = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=(1 << 24) + 1, max_depth=5)
+    assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_spp), fp, out.size, None) == -1
     p_tiles = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=1, max_depth=5, tile_step=2)
     assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_tiles), fp, out.size, None) == -1
     assert lib.rt_camera_setup(0, 9, 20.0, None, None, None, 0.0, 1.0, C.byref(rt_camera())) == -1
@@ -93,6 +100,7 @@ def test_argument_errors():
     bad = rt_scene(-1, None, None, None)
     assert lib.rt_scene_upload(0, C.byref(bad), C.byref(C.c_void_p())) == -1
     assert lib.rt_last_error() != b""
+    assert lib.rt_cache_clear() == 0              # nothing cached without a GPU
 
 
 def test_rows_out():
@@ -116,10 +124,20 @@ def test_rows_out():
 
 def test_version_and_variant():
     import rtclj
+    from rtclj._lib import diag_lib
     assert b"gfx950" in rtclj.lib.rt_version()
-    old = rtclj.lib.rt_set_variant(2)
-    assert rtclj.lib.rt_set_variant(old) == 2
-    assert rtclj.lib.rt_set_variant(99) == old   # ignored
+    # the product build holds the default traversal and its fallbacks only
+    for v in (5, 12, 16, 18):
+        old = rtclj.lib.rt_set_variant(v)
+        assert rtclj.lib.rt_set_variant(old) == v
+    for v in (2, 3, 11, 17, 99, -1):
+        assert rtclj.lib.rt_set_variant(v) == -1 and b"not in this build" in rtclj.lib.rt_last_error()
+    assert rtclj.lib.rt_set_variant(0) == 0
+    # the diagnostic build holds every variant
+    d = diag_lib()
+    for v in range(1, 20):
+        assert d.rt_set_variant(v) >= 0
+    assert d.rt_set_variant(0) == 19
     assert rtclj.lib.rt_resolve_variant(None) == -1
     out4 = (C.c_int * 4)()
     assert rtclj.lib.rt_launch_occupancy(None, None, out4) < 0   # NULL scene: error, no device call
@@ -128,5 +146,5 @@ def test_version_and_variant():
 def test_schedule_switch():
     import rtclj
     assert rtclj.lib.rt_set_schedule(1) == 0      # adaptive is the default
-    assert rtclj.lib.rt_set_schedule(7) == 1      # ignored
+    assert rtclj.lib.rt_set_schedule(7) == -1     # rejected
     assert rtclj.lib.rt_set_schedule(0) == 1

@@ -85,3 +85,19 @@ def test_two_rank_gloo_shards(scaling):
         avg = (parts[0][1] + parts[1][1]) / 2
         assert np.allclose(avg, both, atol=2e-6)
         assert not np.array_equal(parts[0][1], parts[1][1])
+
+
+def test_bench_defaults_to_row_tile_strong_scaling(monkeypatch):
+    """bench.py's N-GPU default is north_star's row-tile shard (strong
+    scaling): rank r of N renders tiles r, r + N, ... of the one frame."""
+    import importlib
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    sys.path.insert(0, str(ROOT))
+    bench = importlib.import_module("bench")
+    a = bench.parse()
+    assert a.scaling == "strong" and a.workload == "c1"
+    from rtclj.shard import shard_params
+    p0 = shard_params(2, 0, 1200, 675, 100, 50, scaling=a.scaling)
+    p1 = shard_params(2, 1, 1200, 675, 100, 50, scaling=a.scaling)
+    assert (p0["tile_first"], p1["tile_first"], p0["tile_step"]) == (0, 1, 2)
+    assert set(bench.WORKLOADS) == {"c1", "c2", "c3", "c4"}

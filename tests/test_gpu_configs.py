@@ -1,0 +1,173 @@
+"""BASELINE.json's configurations at their own sizes on the GPU, and the
+fp64 reference-semantics pin of the benchmark workload.
+
+  C1 cover 1200x675, 100 spp, depth 50: the kernel's frame against the
+     oracle's MODE_REF64 (the Clojure path in double) on every 8th row at
+     full spp, with tests/test_oracle_cover_pin.py's tolerances, and the
+     segments per sample within 2e-3 of REF64's;
+  C2 3840x2160, 500 spp (484 bodies): the whole frame, deterministic,
+     finite, in range, two rows bit-exact against the fp32 mirror;
+  C3 3840x2160, 1000 spp, row tiles over 8 GPUs + host gather: rt_render's
+     8-way fan-out (RT_FLAG_SHARDS_ON_DEVICE0 puts the 8 shards on this box's
+     one GPU) bit-identical to the 1-shard frame;
+  C4 7680x4320, 2000 spp, depth 64, 1000 bodies: the whole frame's
+     properties, a row band re-rendered alone equal to the frame's rows, and
+     a 64-pixel strip bit-exact against the mirror at full spp.
+
+The scene cache of rt_render (include/rt.h) is checked here too: a repeat
+call hits it, a changed body misses it, and neither changes a bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle.pin import compare, within
+
+pytestmark = pytest.mark.gpu
+
+NT = min(16, os.cpu_count() or 1)   # the GPU box's CPU share
+
+
+def _oracle(mode, sc, cam, w, h, spp, depth, rows=None, row_step=1):
+    out, _, segs, smp = oracle.render(mode, sc.sphere.astype(np.float64), sc.kind, sc.mat.astype(np.float64),
+                                      cam.as_list(), cam.defocus, w, h, spp, depth, seed=1, rows=rows,
+                                      row_step=row_step, nthreads=NT)
+    return out, segs, smp
+
+
+def _props(img, st, lo=2.4, hi=3.0):
+    assert np.isfinite(img).all() and img.min() >= 0.0 and img.max() <= 1.0 + 1e-6
+    assert lo < st["segments"] / st["samples"] < hi
+
+
+def _launch_rows(sc, cam, w, h, spp, depth, row_tile, tile_first, tile_step):
+    """rt_launch of an interleaved row selection on a fresh device scene ->
+    (rows array, segments, samples)."""
+    import ctypes as C
+    import torch
+    from rtclj._lib import check, lib, rt_params
+    p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=depth, seed=1,
+                  row_tile=row_tile, tile_first=tile_first, tile_step=tile_step)
+    n = check(lib.rt_rows_out(C.byref(p)))
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    try:
+        out = torch.full((n * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream()
+        check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), C.c_void_p(cnt.data_ptr()),
+                            C.c_void_p(s.cuda_stream)))
+        torch.cuda.synchronize()
+    finally:
+        lib.rt_scene_free(ds)
+    c = cnt.cpu().tolist()
+    return out.cpu().numpy().reshape(n, w, 3), c[0], c[1]
+
+
+def test_c1_against_fp64_reference_semantics(gpu_lib):
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = scenes.cover(11)
+    w, h, spp = 1200, 675, 100
+    cam = scenes.cover_camera(w, h)
+    st = {}
+    g = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=1, stats=st)
+    _props(g, st)
+    # every 8th row on its own (1-row tiles, stride 8): the frame's rows, and
+    # the segment count of exactly those rows
+    rows, segs32, smp32 = _launch_rows(sc, cam, w, h, spp, 50, row_tile=1, tile_first=0, tile_step=8)
+    assert np.array_equal(rows, g[::8])
+    ref, segs, smp = _oracle(oracle.MODE_REF64, sc, cam, w, h, spp, 50, row_step=8)
+    assert ref.shape == (85, w, 3) and smp == smp32
+    s = compare(ref, segs / smp, rows, segs32 / smp32, by=4)
+    ok = within(s)
+    assert all(ok.values()), (ok, s)
+
+
+def test_c2_full_frame(gpu_lib):
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = scenes.cover(11)
+    w, h, spp = 3840, 2160, 500
+    cam = scenes.cover_camera(w, h)
+    st, st2 = {}, {}
+    a = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=1, stats=st)
+    b = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=1, stats=st2)
+    assert np.array_equal(a, b)
+    assert st["samples"] == w * h * spp and st2["scene_cached"] == 1
+    _props(a, st)
+    for r in (1000, 1701):
+        ref, segs, smp = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, 50, rows=(r, r + 1))
+        assert np.array_equal(a[r:r + 1], ref), r
+
+
+def test_c3_eight_shard_fan_out(gpu_lib):
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0
+    sc = scenes.cover(11)
+    w, h, spp = 3840, 2160, 1000
+    cam = scenes.cover_camera(w, h)
+    st1, st8 = {}, {}
+    one = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=1, n_devices=1, stats=st1)
+    eight = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=1, n_devices=8,
+                     flags=RT_FLAG_SHARDS_ON_DEVICE0, stats=st8)
+    assert st8["n_devices"] == 8
+    assert np.array_equal(one, eight)
+    assert st1["samples"] == st8["samples"] == w * h * spp and st1["segments"] == st8["segments"]
+    _props(one, st1)
+
+
+def test_c4_full_frame(gpu_lib):
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    sc = scenes.cover_c4()
+    assert len(sc) == 1000
+    w, h, spp, depth = 7680, 4320, 2000, 64
+    cam = scenes.cover_camera(w, h)
+    st = {}
+    img = R.render(sc, cam, w, h, spp=spp, max_depth=depth, seed=1, stats=st)
+    assert img.shape == (h, w, 3) and st["samples"] == w * h * spp
+    _props(img, st)
+    # a band rendered alone (row_begin offset, other tiling) == the frame's rows
+    band = R.render(sc, cam, w, h, spp=spp, max_depth=depth, seed=1, rows=(2100, 2116))
+    assert np.array_equal(band, img[2100:2116])
+    # a 64-pixel strip of one row, full spp, against the fp32 mirror
+    r = 2500
+    ref, _, _ = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, depth, rows=(r, r + 1))
+    assert np.array_equal(img[r, 3000:3064], ref[0, 3000:3064])
+
+
+def test_scene_cache_hits_and_invalidates(gpu_lib):
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import lib
+    lib.rt_cache_clear()
+    sc = scenes.cover(11)
+    w, h = 200, 112
+    cam = scenes.cover_camera(w, h)
+    s1, s2, s3, s4 = {}, {}, {}, {}
+    a = R.render(sc, cam, w, h, spp=8, seed=2, stats=s1)
+    b = R.render(sc, cam, w, h, spp=8, seed=2, stats=s2)
+    assert s1["scene_cached"] == 0 and s2["scene_cached"] == 1 and np.array_equal(a, b)
+    # a changed body (same count) misses the cache and renders its own scene
+    sph = sc.sphere.copy()
+    sph[-1, 1] += 0.25                     # lift the r = 1 metal body
+    moved = R.Scene(sph, sc.kind, sc.mat)
+    c = R.render(moved, cam, w, h, spp=8, seed=2, stats=s3)
+    assert s3["scene_cached"] == 0 and not np.array_equal(a, c)
+    ref_c, _, _, _ = oracle.render(oracle.MODE_MIRROR32, moved.sphere.astype(np.float64), moved.kind,
+                                   moved.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, 8, 50, seed=2,
+                                   nthreads=NT)
+    assert np.array_equal(c, ref_c)
+    # a material change alone misses too
+    mat = sc.mat.copy()
+    mat[0, :3] = (0.7, 0.1, 0.1)
+    d = R.render(R.Scene(sc.sphere, sc.kind, mat), cam, w, h, spp=8, seed=2, stats=s4)
+    assert s4["scene_cached"] == 0 and not np.array_equal(a, d)
+    # the original is still cached (LRU of 4) and still renders the same bits
+    e = R.render(sc, cam, w, h, spp=8, seed=2, stats=s1)
+    assert s1["scene_cached"] == 1 and np.array_equal(a, e)
+    assert lib.rt_cache_clear() == 3

@@ -18,6 +18,28 @@ TOL_ABS = 1e-4
 TOL_FRAC = 0.995
 
 
+PRODUCT_VARIANTS = (0, 5, 12, 16, 18)
+
+
+class variant:
+    """Select kernel variant v for the block: in the product library when it
+    holds v, else in the diagnostic build.  `as` gives the library to pass to
+    R.render(library=...)."""
+
+    def __init__(self, v):
+        from rtclj._lib import diag_lib, lib
+        self.v = v
+        self.lib = lib if v in PRODUCT_VARIANTS else diag_lib()
+
+    def __enter__(self):
+        self.old = self.lib.rt_set_variant(self.v)
+        assert self.old >= 0, self.lib.rt_last_error()
+        return self.lib
+
+    def __exit__(self, *exc):
+        self.lib.rt_set_variant(self.old)
+
+
 def _ref_scene():
     from rtclj import raytracing as R
     return R.Scene.from_bodies(R.hittables)
@@ -161,47 +183,42 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
-@pytest.mark.parametrize("lpp", [1, 2, 4, -1, -2, -3])
-def test_every_variant_and_launch_shape_is_bit_exact(gpu_lib, variant, lpp):
-    """Kernel variants (table in LDS / scalar cache, simple / grouped scan,
-    stats builds) and lanes-per-pixel launch shapes all give the mirror's bits."""
+@pytest.mark.parametrize("v", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
+def test_every_variant_is_bit_exact(gpu_lib, v):
+    """Kernel variants (product and diagnostic builds: table in LDS / scalar
+    cache, simple / grouped / packed scan, BVH traversals, stats builds) all
+    give the mirror's bits."""
     from rtclj import scenes
     from rtclj import raytracing as R
-    from rtclj._lib import lib
     sc = scenes.cover(11)
-    w, h, spp = 72, 40, 7          # odd spp: unequal stripes (2,2,2,1)
+    w, h, spp = 72, 40, 7
     cam = scenes.cover_camera(w, h)
-    ov, ol = lib.rt_set_variant(variant), lib.rt_set_lanes_per_pixel(lpp)
-    try:
+    with variant(v) as dll:
         st = {}
-        g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st)
-        if variant in (3, 6, 7, 10, 13, 15, 17, 19):
+        g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st, library=dll)
+        if v in (3, 6, 7, 10, 13, 15, 17, 19):
             import ctypes as C
-            d = (C.c_uint64 * 16)()
-            lib.rt_debug_stats(d)
-    finally:
-        lib.rt_set_variant(ov)
-        lib.rt_set_lanes_per_pixel(ol)
+            d = (C.c_uint64 * 32)()
+            assert dll.rt_debug_stats(d) == 0 and d[0] > 0 and d[5] > 0
     ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4)
-    assert np.array_equal(g, ref), f"variant {variant} lpp {lpp}"
+    assert np.array_equal(g, ref), f"variant {v}"
     assert st["segments"] == segs
 
 
-@pytest.mark.parametrize("spp", [1, 2, 3, 4, 5, 100])
-def test_sample_stripes_edge_spp(gpu_lib, spp):
+@pytest.mark.parametrize("spp", [1, 2, 3, 4, 5, 63, 100, 8191, 8192, 12288])
+def test_edge_spp(gpu_lib, spp):
+    """spp around the pool's index arithmetic: multiply-high division up to
+    8191 samples per pixel, exact integer division above (the round-1
+    multiply-high was inexact there)."""
     from rtclj import raytracing as R
-    from rtclj._lib import lib
     sc = _ref_scene()
-    cam = R.camera(40, 22, **R.REFERENCE_CAMERA)
-    ref, _, _ = _mirror(sc, cam, 40, 22, spp, 20, seed=8)
-    for lpp in (0, 1, 2, 4, -1, -2, -3):
-        old = lib.rt_set_lanes_per_pixel(lpp)
-        try:
-            g = R.render(sc, cam, 40, 22, spp=spp, max_depth=20, seed=8)
-        finally:
-            lib.rt_set_lanes_per_pixel(old)
-        assert np.array_equal(g, ref), (spp, lpp)
+    w, h = (40, 22) if spp <= 100 else (9, 10)   # 9 x 10: a ragged tile in both directions
+    cam = R.camera(w, h, **R.REFERENCE_CAMERA)
+    st = {}
+    g = R.render(sc, cam, w, h, spp=spp, max_depth=20, seed=8, stats=st)
+    ref, segs, smp = _mirror(sc, cam, w, h, spp, 20, seed=8)
+    assert np.array_equal(g, ref), spp
+    assert st["segments"] == segs and st["samples"] == smp == w * h * spp
 
 
 def test_max_spheres_and_too_many(gpu_lib):
@@ -280,8 +297,8 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("variant", [11, 12, 14, 16, 18])
-def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
+@pytest.mark.parametrize("v", [11, 12, 14, 16, 18])
+def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, v):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
     from rtclj import raytracing as R
@@ -291,15 +308,12 @@ def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, variant):
              (scenes.cover(16), scenes.cover_camera(640, 360), 640, 360, 16),
              (_ref_scene(), R.camera(400, 225, **R.REFERENCE_CAMERA), 400, 225, 100)]
     for sc, cam, w, h, spp in cases:
-        old = lib.rt_set_variant(5)
-        try:
+        with variant(5) as dll:
             st_a = {}
-            a = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_a)
-            lib.rt_set_variant(variant)
+            a = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_a, library=dll)
+        with variant(v) as dll:
             st_b = {}
-            b = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_b)
-        finally:
-            lib.rt_set_variant(old)
+            b = R.render(sc, cam, w, h, spp=spp, seed=1, stats=st_b, library=dll)
         assert np.array_equal(a, b), (w, h, int((a != b).any(axis=-1).sum()))
         assert st_a["segments"] == st_b["segments"]
 
@@ -315,11 +329,8 @@ def test_bvh_axis_aligned_rays(gpu_lib):
     cam = R.camera(65, 37, 60.0, (0.0, 1.0, 12.0), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), 0.0, 12.0)
     out = {}
     for v in (5, 11, 16):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 65, 37, spp=64, seed=3)
-        finally:
-            lib.rt_set_variant(old)
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 65, 37, spp=64, seed=3, library=dll)
     assert np.array_equal(out[5], out[11])
     assert np.array_equal(out[5], out[16])
 
@@ -342,11 +353,8 @@ def test_bvh_small_scenes(gpu_lib, n):
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
     out = {}
     for v in (5, 11, 16, 18):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5)
-        finally:
-            lib.rt_set_variant(old)
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5, library=dll)
     assert np.array_equal(out[5], out[11])
     assert np.array_equal(out[5], out[16])
     assert np.array_equal(out[5], out[18])
@@ -378,11 +386,8 @@ def test_bvh_big_bodies(gpu_lib, n_big):
     cam = R.camera(64, 36, **R.REFERENCE_CAMERA)
     out = {}
     for v in (5, 11, 16, 18):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 64, 36, spp=8, max_depth=20, seed=9)
-        finally:
-            lib.rt_set_variant(old)
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 64, 36, spp=8, max_depth=20, seed=9, library=dll)
     for v in (11, 16, 18):
         assert np.array_equal(out[5], out[v]), v
     ref, _, _ = _mirror(sc, cam, 64, 36, 8, 20, seed=9)
@@ -407,11 +412,8 @@ def test_bvh_cover16_u8_stack_and_u16_indices(gpu_lib):
         lib.rt_scene_free(ds)
     out = {}
     for v in (5, 16, 18):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 96, 54, spp=6, max_depth=64, seed=4)
-        finally:
-            lib.rt_set_variant(old)
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 96, 54, spp=6, max_depth=64, seed=4, library=dll)
     assert np.array_equal(out[5], out[16])
     assert np.array_equal(out[5], out[18])
     ref, _, _ = _mirror(sc, cam, 96, 54, 6, 64, seed=4)
@@ -446,16 +448,13 @@ def test_bvh_8body_tree_over_256_nodes_uses_4body(gpu_lib):
         lib.rt_scene_free(ds)
     out = {}
     for v in (5, 18):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 64, 36, spp=4, max_depth=10, seed=2)
-        finally:
-            lib.rt_set_variant(old)
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 64, 36, spp=4, max_depth=10, seed=2, library=dll)
     assert np.array_equal(out[5], out[18])
 
 
-@pytest.mark.parametrize("variant", [0, 11, 16, 18])
-def test_bvh_large_scene_falls_back(gpu_lib, variant):
+@pytest.mark.parametrize("vsel", [0, 11, 16, 18])
+def test_bvh_large_scene_falls_back(gpu_lib, vsel):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
     the global-memory traversal of the 2-body tree: same bits as the scan."""
     from rtclj import raytracing as R
@@ -472,13 +471,10 @@ def test_bvh_large_scene_falls_back(gpu_lib, variant):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(96, 54, 40.0, (0, 1, 3), (0, 1, -10), (0, 1, 0), 0.0, 10.0)
     out = {}
-    for v in (5, variant):
-        old = lib.rt_set_variant(v)
-        try:
-            out[v] = R.render(sc, cam, 96, 54, spp=4, max_depth=10, seed=2)
-        finally:
-            lib.rt_set_variant(old)
-    assert np.array_equal(out[5], out[variant])
+    for v in (5, vsel):
+        with variant(v) as dll:
+            out[v] = R.render(sc, cam, 96, 54, spp=4, max_depth=10, seed=2, library=dll)
+    assert np.array_equal(out[5], out[vsel])
 
 
 def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
@@ -488,8 +484,8 @@ def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
     return out, segs, smp
 
 
-@pytest.mark.parametrize("variant", [0, 5, 11, 16, 18])
-def test_realm_flag_matches_mirror(gpu_lib, variant):
+@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18])
+def test_realm_flag_matches_mirror(gpu_lib, vsel):
     """RT_FLAG_REALM (realm.raytracing semantics) through the kernel == the
     oracle's MODE_REALM32, bit for bit: the realm scene and the cover scene."""
     from rtclj import raytracing as R
@@ -497,16 +493,13 @@ def test_realm_flag_matches_mirror(gpu_lib, variant):
     from rtclj._lib import lib
     cases = [(R.Scene.from_bodies(realm.hittables), realm.camera(48, 27), 48, 27, 8),
              (scenes.cover(11), scenes.cover_camera(40, 22), 40, 22, 7)]
-    old = lib.rt_set_variant(variant)
-    try:
+    with variant(vsel) as dll:
         for sc, cam, w, h, spp in cases:
             st = {}
-            g = realm.render(sc, cam, w, h, spp=spp, max_depth=50, seed=3, stats=st)
+            g = realm.render(sc, cam, w, h, spp=spp, max_depth=50, seed=3, stats=st, library=dll)
             ref, segs, smp = _realm_mirror(sc, cam, w, h, spp, 50, seed=3)
-            assert np.array_equal(g, ref), (variant, w, h)
+            assert np.array_equal(g, ref), (vsel, w, h)
             assert st["segments"] == segs and st["samples"] == smp
-    finally:
-        lib.rt_set_variant(old)
 
 
 def test_realm_shards_and_fixture(gpu_lib):

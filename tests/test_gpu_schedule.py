@@ -27,9 +27,11 @@ def env(gpu_lib):
 
 
 def _launch(env, cam, w, h, spp, stream=None, seed=1, rows=None, row_tile=0, tile_first=0, tile_step=0,
-            sample_begin=0):
-    sc, ds, torch = env
+            sample_begin=0, dll=None, ds=None):
+    sc, ds0, torch = env
     from rtclj._lib import check, lib, rt_params
+    ds = ds if ds is not None else ds0
+    dll = dll if dll is not None else lib
     r0, r1 = rows or (0, h)
     p = rt_params(width=w, height=h, row_begin=r0, row_end=r1, spp=spp, max_depth=50, seed=seed,
                   sample_begin=sample_begin, row_tile=row_tile, tile_first=tile_first, tile_step=tile_step)
@@ -38,8 +40,8 @@ def _launch(env, cam, w, h, spp, stream=None, seed=1, rows=None, row_tile=0, til
     with torch.cuda.stream(s):
         out = torch.full((n * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
     s.synchronize()
-    check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), None,
-                        C.c_void_p(s.cuda_stream)))
+    rc = dll.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), None, C.c_void_p(s.cuda_stream))
+    assert rc == 0, dll.rt_last_error()
     s.synchronize()
     return out.cpu().numpy().reshape(n, w, 3)
 
@@ -49,23 +51,30 @@ def _render(sc, cam, w, h, spp, **kw):
     return R.render(sc, cam, w, h, spp=spp, max_depth=50, **kw)
 
 
-@pytest.mark.parametrize("variant,lpp", [(0, 0), (0, 1), (0, 4), (11, 0), (18, 2), (5, 0), (0, -1), (18, -1), (0, -2), (11, -2), (0, -3), (18, -3)])
-def test_repeated_launches_are_bit_identical(env, variant, lpp):
+@pytest.mark.parametrize("v", [0, 5, 12, 16, 18, 11, 14])
+def test_repeated_launches_are_bit_identical(env, v):
     from rtclj import scenes
-    from rtclj._lib import lib
+    from rtclj._lib import diag_lib, lib
     sc = env[0]
     w, h, spp = 333, 187, 6                       # ragged tiles at both edges
     cam = scenes.cover_camera(w, h)
-    ov, ol = lib.rt_set_variant(variant), lib.rt_set_lanes_per_pixel(lpp)
+    want = _render(sc, cam, w, h, spp)
+    dll = lib if v in (0, 5, 12, 16, 18) else diag_lib()
+    ds = env[1]
+    if dll is not lib:                            # the diagnostic build's own device scene
+        ds = C.c_void_p()
+        from rtclj._lib import check
+        check(dll.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    old = dll.rt_set_variant(v)
     try:
-        want = _render(sc, cam, w, h, spp)
         for k in range(4):                        # launch 0 plain, then scheduled by the previous launch
-            got = _launch(env, cam, w, h, spp)
+            got = _launch(env, cam, w, h, spp, dll=dll, ds=ds)
             assert not np.isnan(got).any(), k
             assert np.array_equal(got, want), k
     finally:
-        lib.rt_set_variant(ov)
-        lib.rt_set_lanes_per_pixel(ol)
+        dll.rt_set_variant(old)
+        if dll is not lib:
+            dll.rt_scene_free(ds)
 
 
 def test_schedule_off_matches_on(env):
@@ -148,30 +157,17 @@ def test_streams_keep_separate_records(env):
         assert np.array_equal(o.cpu().numpy().reshape(h, w, 3), want)
 
 
-@pytest.mark.parametrize("lpp", [-1, -2, -3])
-@pytest.mark.parametrize("spp,pool_bytes", [(10, 3), (7, 1), (9, 4), (1, 0), (3, 0)])
-def test_sample_pool_rounds(env, monkeypatch, spp, pool_bytes, lpp):
-    """The sample pools (rt_set_lanes_per_pixel(-1 / -2 / -3): 4x4 / 8x8 pixels
-    per wave, 8x8 per workgroup) in several rounds (scratch limited through RTCLJ_POOL_BYTES to
-    `pool_bytes` samples per pixel; 9 spp in rounds of 4 ends stripes inside
-    and at round ends), and with spp < 4: the stripe contract's bits, via
-    rt_launch and rt_render."""
+@pytest.mark.parametrize("spp", [1, 3, 9, 8191, 8193])
+def test_large_and_small_spp_launches(env, spp):
+    """One launch per frame at any spp (the fixed-point sums need no rounds):
+    rt_launch on a persistent scene == rt_render, at spp around the
+    multiply-high / integer-division switch of the pool index."""
     from rtclj import scenes
-    from rtclj._lib import lib
     sc = env[0]
-    w, h = 150, 77
+    w, h = (150, 77) if spp < 100 else (10, 9)
     cam = scenes.cover_camera(w, h)
-    want = _render(sc, cam, w, h, spp)             # default launch shape (stripes)
-    t = 16 if lpp == -2 else 8
-    tiles = ((w + t - 1) // t) * ((h + t - 1) // t)
-    if pool_bytes:
-        monkeypatch.setenv("RTCLJ_POOL_BYTES", str(tiles * 4 * (64 if lpp == -2 else 16) * 12 * pool_bytes))
-    old = lib.rt_set_lanes_per_pixel(lpp)
-    try:
-        for _ in range(2):
-            got = _launch(env, cam, w, h, spp)
-            assert not np.isnan(got).any()
-            assert np.array_equal(got, want)
-        assert np.array_equal(_render(sc, cam, w, h, spp), want)
-    finally:
-        lib.rt_set_lanes_per_pixel(old)
+    want = _render(sc, cam, w, h, spp)
+    for _ in range(2):
+        got = _launch(env, cam, w, h, spp)
+        assert not np.isnan(got).any()
+        assert np.array_equal(got, want)

@@ -22,13 +22,14 @@ sys.path.insert(0, str(ROOT / "raytracing-clj_amd"))
 import numpy as np  # noqa: E402
 
 from rtclj import raytracing as R, scenes  # noqa: E402
-from rtclj._lib import check, lib  # noqa: E402
+from rtclj._lib import check, diag_lib  # noqa: E402
+
+lib = diag_lib()   # the diagnostic build holds every variant (same ABI, same bits)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", nargs="+", default=["1", "2"],
-                    help="variant[:lanes-per-pixel], e.g. 5 5:2 4:4 7:4")
+    ap.add_argument("--variants", nargs="+", default=["16", "18"], help="kernel variants, e.g. 16 17 11")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--width", type=int, default=1200)
     ap.add_argument("--spp", type=int, default=100)
@@ -60,7 +61,7 @@ def main():
             check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), None,
                                 C.c_void_p(stream.cuda_stream)))
             if v in (3, 6, 7, 10, 13, 15, 17, 19):
-                check(lib.rt_debug_stats((C.c_uint64 * 16)()))   # count the timed launch only
+                check(lib.rt_debug_stats((C.c_uint64 * 32)()))   # count the timed launch only
             cnt.zero_()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -71,20 +72,19 @@ def main():
             st["kernel_ms"] = e0.elapsed_time(e1)
             st["segments"], st["samples"] = int(cnt[0]), int(cnt[1])
             return out.cpu().numpy().reshape(h, w, 3)
-    cfgs = [(int(x.split(":")[0]), int(x.split(":")[1]) if ":" in x else 0) for x in a.variants]
+    cfgs = [int(x) for x in a.variants]
     names = a.variants
     times = {v: [] for v in names}
     ref = None
     stats = {}
     for r in range(a.rounds):
-        for name, (v, lpp) in zip(names, cfgs):
-            lib.rt_set_variant(v)
-            lib.rt_set_lanes_per_pixel(lpp)
+        for name, v in zip(names, cfgs):
+            check(lib.rt_set_variant(v))
             st = {}
             if a.persistent:
                 img = launch(v, st)
             else:
-                img = R.render(sc, cam, w, h, spp=a.spp, max_depth=a.depth, seed=1, stats=st)
+                img = R.render(sc, cam, w, h, spp=a.spp, max_depth=a.depth, seed=1, stats=st, library=lib)
             times[name].append(st["kernel_ms"])
             stats[name] = st
             if ref is None:
@@ -93,14 +93,14 @@ def main():
                 print(f"variant {name}: frame differs from variant {names[0]}!", flush=True)
                 sys.exit(1)
             if v in (3, 6, 7, 10, 13, 15, 17, 19):
-                d = (C.c_uint64 * 16)()
+                d = (C.c_uint64 * 32)()
                 check(lib.rt_debug_stats(d))
                 d = list(d)
                 stats["dbg"] = d
                 stats["dbg_variant"] = name
                 nw = int(d[5])
                 wv = np.zeros(4 * 65536, np.uint64)
-                check(lib.rt_debug_waves(wv.ctypes.data_as(C.POINTER(C.c_uint64)), 65536))
+                check(lib.rt_debug_waves(0, wv.ctypes.data_as(C.POINTER(C.c_uint64)), 65536))
                 stats["waves"] = wv.reshape(-1, 4)[:nw].copy()
     out = {"workload": f"{a.scene} {w}x{h} spp{a.spp} depth{a.depth}", "variants": {}}
     samples = w * h * a.spp
@@ -114,7 +114,7 @@ def main():
     if "dbg" in stats:
         it, lanes, sph, blk, blk_lanes, waves = stats["dbg"][:6]
         segs_total = stats[names[0]]["segments"]
-        if stats["dbg_variant"].split(":")[0] in ("13", "15", "17", "19"):
+        if stats["dbg_variant"] in ("13", "15", "17", "19"):
             tw, tl = stats["dbg"][6], stats["dbg"][7]
             print(json.dumps({"bvh_nodes_per_segment": sph / segs_total, "bvh_leaves_per_segment": blk / segs_total,
                               "bvh_considers_per_segment": blk_lanes / segs_total,

@@ -1,23 +1,47 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 counter CSVs of the timed trace kernel (not its stats
-build, `...true>`): tools/pmc_summary.py DIR [DIR ...]"""
-import collections
-import csv
-import glob
-import sys
+"""Summarise committed rocprofv3 PMC passes (profiles/pmc.sh) of the product
+kernel: per-dispatch averages of every counter over trace_kernel<..., false>
+launches, plus the derived VALU / occupancy / HBM figures bench.py reports.
 
-for d in sys.argv[1:]:
-    agg = collections.defaultdict(list)
-    dur = []
-    for f in glob.glob(f"{d}/*/prof_counter_collection.csv"):
+  python tools/pmc_summary.py profiles/r02/pmc_c1 [kernel_stats.csv]
+"""
+import csv
+import sys
+from pathlib import Path
+
+
+def main():
+    d = Path(sys.argv[1])
+    acc = {}
+    for f in sorted(d.glob("*.csv")):
         for r in csv.DictReader(open(f)):
             if "trace_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for f in glob.glob(f"{d}/*/prof_kernel_stats.csv"):
-        for r in csv.DictReader(open(f)):
-            if "trace_kernel" in r["Name"] and "false>" in r["Name"]:
-                dur.append(float(r["AverageNs"]))
-    print(f"== {d}  kernel avg {sum(dur) / max(len(dur), 1) / 1e6:.2f} ms")
-    for k in sorted(agg):
-        v = agg[k]
-        print(f"  {k:26s} {sum(v) / len(v):.4g}")
+                acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    avg = {k: sum(v) / len(v) for k, v in acc.items()}
+    lines = [f"== {d}  (per-dispatch averages over the product kernel's launches)"]
+    for k in sorted(avg):
+        lines.append(f"  {k:26s} {avg[k]:.4g}")
+    g = avg.get("GRBM_GUI_ACTIVE")
+    if g:
+        cyc = g / 8
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            lines.append(f"  issue_busy   = SQ_ACTIVE_INST_VALU*4/1024 / (GRBM_GUI_ACTIVE/8) = "
+                         f"{avg['SQ_ACTIVE_INST_VALU'] * 4 / 1024 / cyc:.3f}")
+        if "SQ_WAVE_CYCLES" in avg:
+            lines.append(f"  waves/SIMD   = SQ_WAVE_CYCLES*4/1024 / (GRBM_GUI_ACTIVE/8) = "
+                         f"{avg['SQ_WAVE_CYCLES'] * 4 / 1024 / cyc:.3f}")
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_INSTS_VALU" in avg:
+        lines.append(f"  lanes_active = SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU / 64 = "
+                     f"{avg['SQ_THREAD_CYCLES_VALU'] / avg['SQ_INSTS_VALU'] / 64:.3f}")
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        lines.append(f"  HBM bytes/launch = FETCH_SIZE*2 + WRITE_SIZE (KB units) = "
+                     f"{(2 * avg['FETCH_SIZE'] + avg['WRITE_SIZE']) * 1024 / 1e6:.3f} MB")
+    if len(sys.argv) > 2:
+        for r in csv.DictReader(open(sys.argv[2])):
+            if "trace_kernel" in r.get("Name", ""):
+                lines.append(f"  kernel {r['Name'][:60]}: calls {r['Calls']} avg {float(r['AverageNs']) / 1e6:.3f} ms")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
