@@ -19,6 +19,7 @@
  */
 #include <jni.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/rt.h"
@@ -48,12 +49,21 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
     return RT_E_ARG;
   }
   const jsize out_len = (*env)->GetArrayLength(env, out_rgb);
-  /* copy the small inputs; pin only the framebuffer (no JNI calls while it is pinned) */
+  /* Copy every input; render into a malloc'd buffer and copy it back with
+   * SetFloatArrayRegion.  Nothing is pinned while rt_render runs (a full
+   * multi-GPU frame can take seconds: a critical section would block GC
+   * JVM-wide for that long). */
   float* sph = (float*)(*env)->GetFloatArrayElements(env, spheres, NULL);
   jint* knd = (*env)->GetIntArrayElements(env, kinds, NULL);
   float* mat = (float*)(*env)->GetFloatArrayElements(env, mats, NULL);
+  float* out = (float*)malloc((size_t)out_len * sizeof(float) + 1);
   float cam18[18];
   (*env)->GetFloatArrayRegion(env, camera, 0, 18, cam18);
+  int rc = RT_E_ARG;
+  if (!sph || !knd || !mat || !out || (*env)->ExceptionCheck(env)) {
+    rc = RT_E_ARG; /* an OutOfMemoryError may already be pending */
+    goto done;
+  }
   rt_camera cam;
   memcpy(cam.center, cam18 + 0, 12);
   memcpy(cam.p00, cam18 + 3, 12);
@@ -74,13 +84,14 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   p.seed = (uint64_t)seed;
   p.n_devices = n_gpus;
   p.flags = flags;
-  float* out = (float*)(*env)->GetPrimitiveArrayCritical(env, out_rgb, NULL);
-  const int rc = rt_render(&scene, &cam, &p, out, (size_t)out_len, NULL);
-  (*env)->ReleasePrimitiveArrayCritical(env, out_rgb, out, 0);
-  (*env)->ReleaseFloatArrayElements(env, spheres, (jfloat*)sph, JNI_ABORT);
-  (*env)->ReleaseIntArrayElements(env, kinds, knd, JNI_ABORT);
-  (*env)->ReleaseFloatArrayElements(env, mats, (jfloat*)mat, JNI_ABORT);
-  if (rc < 0) throw_rt(env, rc);
+  rc = rt_render(&scene, &cam, &p, out, (size_t)out_len, NULL);
+  if (rc >= 0) (*env)->SetFloatArrayRegion(env, out_rgb, 0, out_len, out);
+done:
+  free(out);
+  if (sph) (*env)->ReleaseFloatArrayElements(env, spheres, (jfloat*)sph, JNI_ABORT);
+  if (knd) (*env)->ReleaseIntArrayElements(env, kinds, knd, JNI_ABORT);
+  if (mat) (*env)->ReleaseFloatArrayElements(env, mats, (jfloat*)mat, JNI_ABORT);
+  if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_rt(env, rc);
   return rc;
 }
 
@@ -112,9 +123,9 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_writePng(JNIEnv* env, jclass cls, jstri
   }
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
   jbyte* px = (*env)->GetByteArrayElements(env, rgb, NULL);
-  const int rc = rt_write_png(p, (const uint8_t*)px, width, height);
-  (*env)->ReleaseByteArrayElements(env, rgb, px, JNI_ABORT);
-  (*env)->ReleaseStringUTFChars(env, path, p);
+  const int rc = (p && px) ? rt_write_png(p, (const uint8_t*)px, width, height) : RT_E_ARG;
+  if (px) (*env)->ReleaseByteArrayElements(env, rgb, px, JNI_ABORT);
+  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
   if (rc < 0) throw_rt(env, rc);
   return rc;
 }
@@ -123,9 +134,9 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_ppmToPng(JNIEnv* env, jclass cls, jstri
   (void)cls;
   const char* s = (*env)->GetStringUTFChars(env, src, NULL);
   const char* d = (*env)->GetStringUTFChars(env, dst, NULL);
-  const int rc = rt_ppm_to_png(s, d);
-  (*env)->ReleaseStringUTFChars(env, dst, d);
-  (*env)->ReleaseStringUTFChars(env, src, s);
+  const int rc = (s && d) ? rt_ppm_to_png(s, d) : RT_E_ARG;
+  if (d) (*env)->ReleaseStringUTFChars(env, dst, d);
+  if (s) (*env)->ReleaseStringUTFChars(env, src, s);
   if (rc < 0) throw_rt(env, rc);
   return rc;
 }
