@@ -209,7 +209,12 @@ int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out);
 int rt_scene_free(rt_dscene* ds);
 /* Asynchronous: enqueue one trace launch on hip_stream (NULL = default
  * stream) of ds's device.  d_out: device buffer of rt_rows_out(p) x width x 3
- * floats.  d_counters: NULL or device u64[2] += {segments, samples}. */
+ * floats.  d_counters: NULL or device u64[2] += {segments, samples}.
+ * A launch of fewer 8 x 8 tiles than 3 x the workgroups the device holds at
+ * once (a multi-GPU shard, a small frame) splits every tile's samples over
+ * several workgroups; their integer pixel sums are added by a second kernel
+ * on the same stream, from a scratch buffer the library keeps per scene and
+ * stream (splits x rows x width x 3 x 8 bytes).  Bits never depend on it. */
 int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
 

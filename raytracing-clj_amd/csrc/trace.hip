@@ -78,10 +78,17 @@ struct alignas(16) KArgs {
   int n_big_leaves;
   int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
-  const int* tile_order;   // nullable: dispatch slot -> tile (blockIdx.y*gridDim.x + blockIdx.x order)
-  unsigned* tile_cost;     // nullable: per tile, the longest of its waves' durations (s_memrealtime ticks)
+  const int* tile_order;   // nullable: tile order (longest first) -> tile
+  unsigned* tile_cost;     // nullable: per tile, its workgroups' durations summed (s_memrealtime ticks)
+  // Work units: the first n_whole tiles of the order are one
+  // workgroup each, every later tile is `split` workgroups, one contiguous
+  // sample range each, whose integer pixel sums go to part[split index]
+  // (finalize_kernel adds them up)
+  unsigned long long* part;  // [split][rows_out][width][3]
+  int tiles_x;               // 8 x 8 tiles per tile row
+  int n_whole, split;
+  int split_k0[65];          // first sample of each split (split_k0[split] = spp)
   int spp, sample_begin, max_depth;
-  uint32_t spp_magic;    // ceil(2^32 / spp) for j / spp by multiply-high (0: spp == 1 or too large)
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
 };
@@ -255,10 +262,19 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
 
   const int lane = threadIdx.x & 63;
-  // the block's tile: its dispatch slot, or the tile_order permutation of it
-  const int slot = static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x);
-  const int tile = a.tile_order ? a.tile_order[slot] : slot;
-  const int tbx = tile % static_cast<int>(gridDim.x), tby = tile / static_cast<int>(gridDim.x);
+  // the block's unit: a whole tile (dispatch slots [0, n_whole)) or one
+  // sample split of a tile at the order's end
+  const int slot = static_cast<int>(blockIdx.x);
+  int pos = slot, split_ix = 0;
+  const bool split = slot >= a.n_whole;
+  if (split) {
+    const int v = slot - a.n_whole;
+    const int t = v / a.split;
+    pos = a.n_whole + t;
+    split_ix = v - t * a.split;
+  }
+  const int tile = a.tile_order ? a.tile_order[pos] : pos;
+  const int tby = tile / a.tiles_x, tbx = tile - tby * a.tiles_x;
   // the tile's in-image part, vw x vh pixels; pool pixel q at (q % vw, q / vw)
   const int qx0 = tbx * kTile, qy0 = tby * kTile;
   const int vw = max(0, min(kTile, a.width - qx0));
@@ -279,11 +295,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
   uint32_t segs = 0;
 
-  // pool index j -> (pixel q = j / spp, sample k = j % spp); the next free
-  // index is `base`.  j / spp by multiply-high: exact while j * spp < 2^32,
-  // i.e. 64 * spp^2 < 2^32 (the host passes spp_magic = 0 above 8191 and for
-  // spp = 1); q / vw likewise (q < 64, vw <= 8)
-  const int pool = (a.spp > 0 && a.max_depth > 0) ? npx * a.spp : 0;
+  // the unit's samples [k0, k0 + cnt) of each pixel
+  const int k0 = split ? a.split_k0[split_ix] : 0;
+  const int cnt = split ? a.split_k0[split_ix + 1] - k0 : a.spp;
+  // pool index j -> (pixel q = j / cnt, sample k0 + j % cnt); the next free
+  // index is `base`.  j / cnt by multiply-high: exact while j * cnt < 2^32,
+  // i.e. 64 * cnt^2 < 2^32 (cnt <= 8191; integer division above, and for
+  // cnt = 1); q / vw likewise (q < 64, vw <= 8)
+  const uint32_t cnt_magic = (cnt > 1 && cnt <= 8191) ? 0xffffffffu / static_cast<uint32_t>(cnt) + 1u : 0u;
+  const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
   bool active = j < pool;
@@ -314,14 +334,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         }
       }
       // pool index -> (pixel, sample)
-      if (a.spp_magic) q = static_cast<int>(__umulhi(static_cast<uint32_t>(j), a.spp_magic));
-      else q = a.spp == 1 ? j : static_cast<int>(static_cast<uint32_t>(j) / static_cast<uint32_t>(a.spp));
-      k = j - q * a.spp;
+      if (cnt_magic) q = static_cast<int>(__umulhi(static_cast<uint32_t>(j), cnt_magic));
+      else q = cnt == 1 ? j : static_cast<int>(static_cast<uint32_t>(j) / static_cast<uint32_t>(cnt));
+      k = j - q * cnt;
       const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
       const int px = qx0 + (q - qy * vw);
       const int gy = image_row(qy0 + qy);
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
-      st = mix32(pixel_key(px, gy) + static_cast<uint32_t>(a.sample_begin + k) * 0x9e3779b9u);
+      st = mix32(pixel_key(px, gy) + static_cast<uint32_t>(a.sample_begin + k0 + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
       // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
       const float fx = static_cast<float>(px) + rng_centered(st);
@@ -937,15 +957,20 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     const int fp = t / 3, ch = t - 3 * fp;
     const int qy = vw == 1 ? fp : static_cast<int>(__umulhi(static_cast<uint32_t>(fp), mag_vw));
     const int px = qx0 + (fp - qy * vw), ro = qy0 + qy;
-    const float tot = static_cast<float>(s_acc[t]) * 0x1p-24f;   // RN(float(sum)), exact scale
-    const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
-    // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
-    a.out[(static_cast<size_t>(ro) * a.width + px) * 3 + ch] = a.realm ? tot * (1.0f / inv) : tot / inv;
+    const size_t e = (static_cast<size_t>(ro) * a.width + px) * 3 + ch;
+    if (split) {   // one split's integer sum; finalize_kernel adds the splits (order-free)
+      a.part[static_cast<size_t>(split_ix) * a.rows_out * a.width * 3 + e] = s_acc[t];
+    } else {
+      const float tot = static_cast<float>(s_acc[t]) * 0x1p-24f;   // RN(float(sum)), exact scale
+      const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
+      // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
+      a.out[e] = a.realm ? tot * (1.0f / inv) : tot / inv;
+    }
   }
 
-  if (a.tile_cost && lane == 0) {   // the adaptive schedule's measurement
+  if (a.tile_cost && threadIdx.x == 0) {   // the adaptive schedule's measurement: the workgroup's time
     const uint64_t dt = __builtin_amdgcn_s_memrealtime() - st_t0;
-    atomicMax(&a.tile_cost[tile], static_cast<unsigned>(dt < 0xffffffffull ? dt : 0xffffffffull));
+    atomicAdd(&a.tile_cost[tile], static_cast<unsigned>(dt < 0xffffffffull ? dt : 0xffffffffull));
   }
   if constexpr (STATS) {
     if (a.dbg && st_iter) {
@@ -993,7 +1018,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[11], static_cast<unsigned long long>(c3));
     }
     if (a.dbgw && lane == 0) {
-      const size_t wid = static_cast<size_t>(tile) * 4 + (threadIdx.x >> 6);   // by tile
+      const size_t wid = static_cast<size_t>(slot) * 4 + (threadIdx.x >> 6);   // by dispatch slot
       if (wid < 65536) {
         a.dbgw[4 * wid + 0] = st_t0;
         a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1038,6 +1063,30 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += 1024) order[atomicAdd(&cursor[cost_bucket(cost[i])], 1)] = i;
+}
+
+// The split tiles' pixels (order positions [n_whole, n_tiles)): the sum of
+// their splits' integer sums (exact, any order), then the unsplit epilogue's
+// conversion: RN(float(sum)) * 2^-24, / spp (realm: * (1/spp)).  One block
+// per split tile, thread t = tile row * 24 + x * 3 + channel.
+__global__ __launch_bounds__(192) void finalize_kernel(const unsigned long long* __restrict__ part,
+                                                        const int* __restrict__ order, int n_whole, int split,
+                                                        int tiles_x, int width, int rows, float* __restrict__ out,
+                                                        int spp, int realm) {
+  const int pos = n_whole + static_cast<int>(blockIdx.x);
+  const int tile = order ? order[pos] : pos;
+  const int tby = tile / tiles_x, tbx = tile - tby * tiles_x;
+  const int t = static_cast<int>(threadIdx.x);
+  const int row = t / (kTile * 3), col = t - row * (kTile * 3);
+  const int y = tby * kTile + row, x3 = tbx * kTile * 3 + col;
+  if (y >= rows || x3 >= width * 3) return;
+  const size_t n = static_cast<size_t>(rows) * width * 3;
+  const size_t e = static_cast<size_t>(y) * width * 3 + x3;
+  unsigned long long sum = 0;
+  for (int s = 0; s < split; ++s) sum += part[static_cast<size_t>(s) * n + e];
+  const float tot = static_cast<float>(sum) * 0x1p-24f;
+  const float inv = static_cast<float>(spp > 0 ? spp : 1);
+  out[e] = realm ? tot * (1.0f / inv) : tot / inv;
 }
 
 // ------------------------------------------------------------- host ------
@@ -1151,6 +1200,7 @@ struct DTree {
 // stream so that nothing a stream's kernels read is written from another
 // stream; a dscene serves up to kSchedStreams streams this way, launches on
 // further streams run unscheduled.
+// The same per-stream entry holds the split tiles' partial sums (rt_launch).
 struct ScheduleKey {
   int width, rows, row_begin, row_tile, tile_first, tile_step, gx, gy;
 };
@@ -1161,6 +1211,8 @@ struct Schedule {
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
+  unsigned long long* part = nullptr;   // [split][rows][width][3] pixel sums of split tiles
+  size_t part_cap = 0;                  // u64 elements
 };
 constexpr int kSchedStreams = 8;
 struct ScheduleSet {
@@ -1171,6 +1223,7 @@ struct ScheduleSet {
     for (int k = 0; k < used; ++k) {
       if (s[k].cost) (void)hipFree(s[k].cost);
       if (s[k].order) (void)hipFree(s[k].order);
+      if (s[k].part) (void)hipFree(s[k].part);
     }
     used = 0;
   }
@@ -1413,6 +1466,34 @@ static int dbg_buffers(int device, unsigned long long** dbg, unsigned long long*
   return RT_OK;
 }
 
+// Sample split (rt_launch): split every tile of a launch with fewer tiles
+// than kSplitRounds x (resident workgroups), into enough splits to reach that
+// (at most kSplitMax).  tools/shard_time.py on C1's 1/2/4/8-GPU shards
+// (profiles/r02/shard_split_rounds.txt): 3-4 rounds best (8 GPUs: 5.88x at 3,
+// 5.72x at 4, 5.30x at 6, 3.96x at 16; unsplit 2.57x)
+static const int kSplitRounds = [] {
+  const char* e = std::getenv("RTCLJ_SPLIT_ROUNDS");
+  return e ? std::max(1, std::atoi(e)) : 3;
+}();
+constexpr int kSplitMax = 64;
+
+// workgroups device `device` holds at once for kernel fn with `lds` bytes of
+// dynamic LDS (CUs x the occupancy query), cached per (device, fn, lds)
+static int launch_slots(int device, const void* fn, size_t lds) {
+  struct Entry { int device; const void* fn; size_t lds; int slots; };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Entry& e : cache)
+    if (e.device == device && e.fn == fn && e.lds == lds) return e.slots;
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, lds) != hipSuccess)
+    return 0;
+  cache.push_back({device, fn, lds, cus * per});
+  return cus * per;
+}
+
 extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p, float* d_out,
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();
@@ -1447,8 +1528,6 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.spp = p->spp;
   a.sample_begin = p->sample_begin;
   a.max_depth = p->max_depth;
-  // j / spp by multiply-high: exact for j < 64 * spp while 64 * spp^2 <= 2^32
-  a.spp_magic = (p->spp > 1 && p->spp <= 8191) ? static_cast<uint32_t>(0xffffffffu / static_cast<uint32_t>(p->spp)) + 1u : 0u;
   a.realm = (p->flags & RT_FLAG_REALM) ? 1 : 0;
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
@@ -1467,9 +1546,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  const dim3 grid((p->width + kTile - 1) / kTile, (rows + kTile - 1) / kTile);
+  const int gx = (p->width + kTile - 1) / kTile, gy = (rows + kTile - 1) / kTile;
   const dim3 block(256);
-  const int n_tiles = static_cast<int>(grid.x * grid.y);
+  const int n_tiles = gx * gy;
+  a.tiles_x = gx;
   if (v.stats) {
     const int rc = dbg_buffers(ds->device, &a.dbg, &a.dbgw);
     if (rc != RT_OK) return rc;
@@ -1477,11 +1557,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   const size_t lds = launch_lds(*ds, vsel);
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-  // adaptive schedule: dispatch tiles longest first, by the durations the
-  // previous launch of this launch shape on this scene and stream measured
+  // the stream's entry: adaptive schedule and split partial sums
   Schedule* sch = nullptr;
   std::unique_lock<std::mutex> sched_lock;
-  if (g_schedule.load() == 0) {
+  {
     ScheduleSet& set = ds->sched;
     sched_lock = std::unique_lock<std::mutex>(set.mu);
     for (int k = 0; k < set.used && !sch; ++k)
@@ -1491,7 +1570,48 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch->stream = stream;
     }
   }
-  if (sch) {
+  // Sample split: a frame of fewer tiles than
+  // kSplitRounds x the workgroups the GPU holds at once (a shard of a
+  // multi-GPU frame, a small image) runs every tile as `split` workgroups,
+  // one contiguous sample range each, so that the launch does not end on a
+  // few whole tiles running alone (its length would be the longest tile's).
+  // The integer pixel sums add up to the same bits in any grouping.
+  // (The kernel also takes a whole-tile prefix of the order, n_whole; the
+  // split tiles' partial sums go through finalize_kernel.)
+  int split = 1, n_whole = n_tiles;
+  if (sch && p->spp > 1) {
+    if (const char* e = std::getenv("RTCLJ_SPLIT")) {
+      split = std::max(1, std::atoi(e));
+    } else {
+      const int slots = launch_slots(ds->device, v.fn, lds);
+      const int64_t want = static_cast<int64_t>(kSplitRounds) * slots;
+      if (slots > 0 && n_tiles < want) split = static_cast<int>((want + n_tiles - 1) / n_tiles);
+    }
+    split = std::min(split, std::min(p->spp, kSplitMax));
+    if (split > 1) n_whole = 0;
+  }
+  a.split = split;
+  a.n_whole = n_whole;
+  for (int k = 0; k <= split; ++k) a.split_k0[k] = static_cast<int>(static_cast<int64_t>(k) * p->spp / split);
+  const int64_t n_units64 = n_whole + static_cast<int64_t>(n_tiles - n_whole) * split;
+  if (n_units64 > INT_MAX) return set_error(RT_E_ARG, "rt_launch: frame too large");
+  const int n_units = static_cast<int>(n_units64);
+  const size_t n_elems = static_cast<size_t>(rows) * p->width * 3;
+  if (split > 1) {
+    const size_t need = n_elems * split;
+    if (sch->part_cap < need) {   // grow: this stream's kernels may still read the old buffer
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->part) (void)hipFree(sch->part);
+      sch->part = nullptr;
+      sch->part_cap = 0;
+      HIP_TRY(hipMalloc(&sch->part, need * sizeof(unsigned long long)));
+      sch->part_cap = need;
+    }
+    a.part = sch->part;
+  }
+  // adaptive schedule: dispatch tiles longest first, by the durations the
+  // previous launch of this launch shape on this scene and stream measured
+  if (sch && g_schedule.load() == 0) {
     ScheduleKey key{};
     key.width = a.width;
     key.rows = a.rows_out;
@@ -1499,8 +1619,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     key.row_tile = a.row_tile;
     key.tile_first = a.tile_first;
     key.tile_step = a.tile_step;
-    key.gx = static_cast<int>(grid.x);
-    key.gy = static_cast<int>(grid.y);
+    key.gx = gx;
+    key.gy = gy;
     if (std::memcmp(&sch->key, &key, sizeof key) != 0) {
       sch->ready = false;
       sch->key = key;
@@ -1522,8 +1642,17 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
   }
   void* args[] = {&a};
-  HIP_TRY(hipLaunchKernel(v.fn, grid, block, args, lds, stream));
-  if (sch) {
+  HIP_TRY(hipLaunchKernel(v.fn, dim3(n_units), block, args, lds, stream));
+  if (split > 1) {
+    const unsigned long long* part = a.part;
+    const int* order = a.tile_order;
+    int nw = n_whole, sp = split, tx = gx, w = p->width, nr = rows, spp = p->spp, realm = a.realm;
+    float* out = d_out;
+    void* fargs[] = {&part, &order, &nw, &sp, &tx, &w, &nr, &out, &spp, &realm};
+    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&finalize_kernel), dim3(n_tiles - n_whole), dim3(192),
+                            fargs, 0, stream));
+  }
+  if (a.tile_cost) {
     // the next launch's order, stream-ordered after this kernel (no host sync)
     const unsigned* cost = sch->cost;
     int* order = sch->order;

@@ -171,3 +171,60 @@ def test_large_and_small_spp_launches(env, spp):
         got = _launch(env, cam, w, h, spp)
         assert not np.isnan(got).any()
         assert np.array_equal(got, want)
+
+
+@pytest.fixture
+def split_env(monkeypatch):
+    """RTCLJ_SPLIT forces rt_launch's sample split (read at every launch)."""
+    def set_split(k):
+        if k is None:
+            monkeypatch.delenv("RTCLJ_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("RTCLJ_SPLIT", str(k))
+    yield set_split
+    monkeypatch.delenv("RTCLJ_SPLIT", raising=False)
+
+
+@pytest.mark.parametrize("spp", [1, 2, 7, 37, 100, 8193])
+def test_sample_split_is_bit_exact(env, split_env, spp):
+    """Every split of the tiles' samples over workgroups (contiguous sample
+    ranges, integer pixel sums added by finalize_kernel) gives the unsplit
+    frame's bits, including splits > spp (clamped), spp = 1 and per-split
+    counts on both sides of the multiply-high limit."""
+    from rtclj import scenes
+    sc = env[0]
+    w, h = (90, 53) if spp < 1000 else (9, 8)
+    cam = scenes.cover_camera(w, h)
+    split_env(1)
+    want = _launch(env, cam, w, h, spp)
+    assert not np.isnan(want).any()
+    for k in (2, 3, 5, 64, 1000):
+        split_env(k)
+        for _ in range(2):   # the second launch runs the adaptive order of the split units
+            got = _launch(env, cam, w, h, spp)
+            assert np.array_equal(got, want), (spp, k)
+    split_env(None)          # the automatic choice (a small frame: split)
+    assert np.array_equal(_launch(env, cam, w, h, spp), want)
+    assert np.array_equal(_render(sc, cam, w, h, spp), want)
+
+
+def test_sample_split_shards_realm_and_stripes(env, split_env):
+    """Split launches of interleaved row-tile shards, of a sample stripe
+    (sample_begin) and of realm semantics: the unsplit bits."""
+    from rtclj import scenes
+    from rtclj._lib import RT_FLAG_REALM
+    sc = env[0]
+    w, h = 120, 67
+    cam = scenes.cover_camera(w, h)
+    split_env(1)
+    full = _render(sc, cam, w, h, 12)
+    stripe = _launch(env, cam, w, h, 5, sample_begin=7)
+    realm = _render(sc, cam, w, h, 6, flags=RT_FLAG_REALM)
+    for k in (4, 12):
+        split_env(k)
+        for f in range(3):
+            part = _launch(env, cam, w, h, 12, row_tile=8, tile_first=f, tile_step=3)
+            rows = np.concatenate([np.arange(t, min(t + 8, h)) for t in range(8 * f, h, 24)])
+            assert np.array_equal(part, full[rows]), (k, f)
+        assert np.array_equal(_launch(env, cam, w, h, 5, sample_begin=7), stripe), k
+        assert np.array_equal(_render(sc, cam, w, h, 6, flags=RT_FLAG_REALM), realm), k

@@ -42,6 +42,9 @@ static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane;
 static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
 static double g_abs = 0;   // wave iterations with a metal absorption
 static double C_EXACT_B = 32;
+static double C_BALL = 27, C_DISK = 21;   // one rejection-loop trip (random-unit-vec3, disk)
+static int g_restart_k = 32;   // policy 2: shade once this many lanes finished traversal
+static int g_charge_rej = 0;   // policies 0/1: add the rejection trips to the cost (RJ=1)
 
 // VALU wave-instructions per block (from the ISA of the default kernel,
 // trace_kernel<1, 5, -3, false>); leaf and exact costs for NP body pairs per leaf
@@ -78,6 +81,17 @@ struct Trav {
 };
 
 struct Hit { int body; float t; };
+
+// Start-node table (QT=1): a quadtree over the tree's x-z extent; the entry
+// of a level-k cell is the deepest node whose subtree holds every body whose
+// box (grown by QT_M) meets the cell's column (-2: no body).  A ray segment
+// clipped to the root box whose two ends share a level-k cell can start its
+// traversal there.
+static int g_qt = 0, g_qt_res = 32;
+static float g_qt_m = 0.1f;
+static float g_qt_lo[2], g_qt_cell[2];
+static std::vector<std::vector<int>> g_qt_tab;   // per level: res_k x res_k start nodes
+static double g_qt_skip = 0, g_qt_start_depth = 0, g_qt_n = 0;
 
 static int g_candbit = 0;   // the body's position in its leaf (candidate bitmask)
 static void body_test(const float* s, float ox, float oy, float oz, float ux, float uy, float uz,
@@ -123,6 +137,42 @@ static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float u
   };
   int stack[64], sp = 0, node = 0;
   g_segs += 1;
+  if (g_qt) {
+    // the root box = union of node 0's children (centre-relative), padded
+    const BvhNode& r = S.t.nodes[0];
+    float lo[3], hi[3];
+    const float* ax[3] = {r.x, r.y, r.z};
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(ax[k][0], ax[k][1]) - P;
+      hi[k] = std::max(ax[k][2], ax[k][3]) + P;
+    }
+    const float e[3] = {ex, ey, ez}, rr[3] = {rx, ry, rz};
+    float t0 = tmin, t1 = best.t;
+    for (int k = 0; k < 3; ++k) {
+      const float a = (lo[k] - e[k]) * rr[k], b = (hi[k] - e[k]) * rr[k];
+      t0 = std::max(t0, std::min(a, b));
+      t1 = std::min(t1, std::max(a, b));
+    }
+    g_qt_n += 1;
+    if (!(t0 <= t1)) { g_qt_skip += 1; return best; }
+    if (!std::isfinite(t1)) t1 = t0;   // (not reached: the box is finite)
+    int c0[2], c1[2];
+    const float u2[2] = {ux, uz}, e2[2] = {ex, ez};
+    for (int k = 0; k < 2; ++k) {
+      const float a = (e2[k] + u2[k] * t0 - g_qt_lo[k]) / g_qt_cell[k];
+      const float b = (e2[k] + u2[k] * t1 - g_qt_lo[k]) / g_qt_cell[k];
+      c0[k] = std::clamp(int(std::floor(a)), 0, g_qt_res - 1);
+      c1[k] = std::clamp(int(std::floor(b)), 0, g_qt_res - 1);
+    }
+    const unsigned x = unsigned(c0[0] ^ c1[0]) | unsigned(c0[1] ^ c1[1]);
+    const int lvl = x ? 32 - __builtin_clz(x) : 0;
+    if (lvl < int(g_qt_tab.size())) {
+      const int res = g_qt_res >> lvl;
+      const int st = g_qt_tab[lvl][(c0[1] >> lvl) * res + (c0[0] >> lvl)];
+      if (st == -2) { g_qt_skip += 1; return best; }
+      node = st;
+    }
+  }
   for (;;) {
     g_visits += 1;
     const BvhNode& nd = S.t.nodes[node];
@@ -280,6 +330,7 @@ static double wave_cost(const std::vector<const Trav*>& lanes, double* node_step
   g_ball += mball;
   g_both += mboth;
   double c = C_OUT + (g_big_leaves ? g_big_leaves * C_LEAF + exact(mb, ob) : 0.0);
+  if (g_charge_rej) c += C_BALL * mball + C_DISK * md;
   for (size_t i = 0; i < L; ++i) {
     int ml = 0, m1 = 0, m2 = 0, o1 = 0, o2 = 0;
     for (const Trav* t : lanes)
@@ -312,6 +363,95 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
     py = ty * g_tile_h + q / 8;
   };
   R.samples += pool;
+  if (policy == 2) {
+    // lane-level restart: the wave steps the traversal of its lanes until
+    // g_restart_k of them (or all live ones) have finished it, then shades
+    // those lanes and sets up their next segment (camera ray if the path
+    // ended); the others keep their traversal state across the phase
+    struct L { Trav t; size_t i = 0; bool ended = false, live = false; };
+    std::vector<L> st(256);
+    auto setup = [&](int l) {   // trace lane l's next segment (shading applied at its end)
+      Path& p = lanes[l];
+      st[l] = L{};
+      if (p.j < 0) return;
+      int px, py;
+      pixel(p.j, px, py);
+      st[l].ended = step(C, p, px, py, st[l].t);
+      st[l].live = true;
+    };
+    for (int l = 0; l < 256; ++l) setup(l);
+    double wc[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; ++k) {   // first phase: the camera rays' set-up
+      int md = 0, mb = 0, ob = 0;
+      for (int l = 64 * k; l < 64 * k + 64; ++l)
+        if (st[l].live) {
+          md = std::max(md, st[l].t.disk_tries);
+          mb = std::max(mb, __builtin_popcount(st[l].t.big_c));
+          ob |= st[l].t.big_c;
+        }
+      wc[k] += C_OUT * 0.5 + C_DISK * md + (g_big_leaves ? g_big_leaves * C_LEAF + C_EXACT * mb : 0.0);
+    }
+    for (;;) {
+      int w = -1;
+      for (int k = 0; k < 4; ++k) {
+        bool any = false;
+        for (int l = 0; l < 64; ++l) any |= st[64 * k + l].live;
+        if (any && (w < 0 || wc[k] < wc[w])) w = k;
+      }
+      if (w < 0) break;
+      L* ln = &st[64 * w];
+      int nlive = 0, nready = 0;
+      for (int l = 0; l < 64; ++l) {
+        nlive += ln[l].live;
+        nready += ln[l].live && ln[l].i >= ln[l].t.leaves.size();
+      }
+      const int K = std::min(g_restart_k, nlive);
+      double c = 0;
+      while (nready < K) {
+        int ml = 0, m1 = 0, m2 = 0, trav = 0;
+        for (int l = 0; l < 64; ++l) {
+          L& x = ln[l];
+          if (!x.live || x.i >= x.t.leaves.size()) continue;
+          ++trav;
+          ml = std::max<int>(ml, x.t.leaves[x.i]);
+          m1 = std::max(m1, __builtin_popcount(x.t.c1[x.i]));
+          m2 = std::max(m2, __builtin_popcount(x.t.c2[x.i]));
+          ++x.i;
+          R.lane_steps += 1;
+          if (x.i >= x.t.leaves.size()) ++nready;
+        }
+        c += C_NODE + 4 + C_LEAF * ml + C_EXACT * (m1 + m2);   // +4: the ready-count ballot
+        R.steps += 1;
+        g_leaf_passes += ml;
+        g_exact_passes += m1 + m2;
+      }
+      // shading phase of the ready lanes, then their next segments' set-up
+      int mball = 0, md = 0, mb = 0, ob = 0;
+      for (int l = 0; l < 64; ++l) {
+        L& x = ln[l];
+        if (!x.live || x.i < x.t.leaves.size()) continue;
+        mball = std::max(mball, x.t.ball_tries);
+        const int gl = 64 * w + l;
+        if (x.ended) {
+          lanes[gl] = Path{};
+          lanes[gl].j = next < pool ? next++ : -1;
+        }
+        setup(gl);
+        if (st[gl].live) {
+          md = std::max(md, st[gl].t.disk_tries);
+          mb = std::max(mb, __builtin_popcount(st[gl].t.big_c));
+          ob |= st[gl].t.big_c;
+        }
+      }
+      g_ball += mball;
+      g_disk += md;
+      c += C_OUT + C_BALL * mball + C_DISK * md + (g_big_leaves ? g_big_leaves * C_LEAF + C_EXACT * mb : 0.0);
+      wc[w] += c;
+      R.cost += c;
+      R.iters += 1;
+    }
+    return;
+  }
   if (policy == 0) {
     // 4 independent waves, advanced in order of accumulated cost
     double wc[4] = {0, 0, 0, 0};
@@ -364,6 +504,7 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
         }
       auto key = [&](const Path& p) -> int {
         if (key_mode == 3) return oracle_len[&p - lanes.data()];
+        if (key_mode == 4) return 0;   // compaction only
         if (p.fresh) return 0;   // camera rays first (coherent already)
         const int oct = (p.d[0] < 0) | ((p.d[1] < 0) << 1) | ((p.d[2] < 0) << 2);
         if (key_mode == 1) return 1 + oct;
@@ -412,6 +553,66 @@ int main(int argc, char** argv) {
   bvh_build(S.sph.data(), S.n, &S.t, ls, true);
   set_leaf_costs(ls / 2);
   g_big_leaves = S.t.n_big_leaves;
+  if (std::getenv("QT")) {
+    g_qt = std::atoi(std::getenv("QT"));
+    if (std::getenv("QTR")) g_qt_res = std::atoi(std::getenv("QTR"));
+    if (std::getenv("QTM")) g_qt_m = std::atof(std::getenv("QTM"));
+    const int nn = int(S.t.nodes.size());
+    std::vector<int> parent(nn, -1), depth(nn, 0);
+    std::vector<int> holder(S.n, -1);
+    const int np = S.t.leaf_size / 2;
+    for (int i = 0; i < nn; ++i)
+      for (int c = 0; c < 2; ++c) {
+        const int ch = S.t.nodes[i].child[c];
+        if (ch >= 0) parent[ch] = i;
+        else
+          for (int q = 0; q < np; ++q)
+            for (int j = 0; j < 2; ++j) {
+              const int id = S.t.pidx[2 * (~ch + q) + j];
+              if (id >= 0) holder[id] = i;
+            }
+      }
+    for (int i = 1; i < nn; ++i) { int d = 0; for (int k = i; k > 0; k = parent[k]) ++d; depth[i] = d; }
+    auto lca = [&](int a, int b) {
+      if (a < 0) return b;
+      while (depth[a] > depth[b]) a = parent[a];
+      while (depth[b] > depth[a]) b = parent[b];
+      while (a != b) { a = parent[a]; b = parent[b]; }
+      return a;
+    };
+    float lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+    for (int i = 0; i < S.n; ++i) {
+      if (holder[i] < 0) continue;
+      const float* b = &S.sph[4 * i];
+      lo[0] = std::min(lo[0], b[0] - b[3] - S.t.center[0]); hi[0] = std::max(hi[0], b[0] + b[3] - S.t.center[0]);
+      lo[1] = std::min(lo[1], b[2] - b[3] - S.t.center[2]); hi[1] = std::max(hi[1], b[2] + b[3] - S.t.center[2]);
+    }
+    for (int k = 0; k < 2; ++k) {
+      g_qt_lo[k] = lo[k] - g_qt_m;
+      g_qt_cell[k] = (hi[k] - lo[k] + 2 * g_qt_m) / g_qt_res;
+    }
+    for (int res = g_qt_res, lvl = 0; res >= 1; res >>= 1, ++lvl) {
+      std::vector<int> tab(res * res, -2);
+      const float cw = g_qt_cell[0] * (g_qt_res / res), ch = g_qt_cell[1] * (g_qt_res / res);
+      for (int i = 0; i < S.n; ++i) {
+        if (holder[i] < 0) continue;
+        const float* b = &S.sph[4 * i];
+        const float bx0 = b[0] - b[3] - S.t.center[0] - g_qt_m, bx1 = b[0] + b[3] - S.t.center[0] + g_qt_m;
+        const float bz0 = b[2] - b[3] - S.t.center[2] - g_qt_m, bz1 = b[2] + b[3] - S.t.center[2] + g_qt_m;
+        const int x0 = std::max(0, int(std::floor((bx0 - g_qt_lo[0]) / cw))), x1 = std::min(res - 1, int(std::floor((bx1 - g_qt_lo[0]) / cw)));
+        const int z0 = std::max(0, int(std::floor((bz0 - g_qt_lo[1]) / ch))), z1 = std::min(res - 1, int(std::floor((bz1 - g_qt_lo[1]) / ch)));
+        for (int z = z0; z <= z1; ++z)
+          for (int x = x0; x <= x1; ++x) {
+            int& t = tab[z * res + x];
+            t = lca(t == -2 ? -1 : t, holder[i]);
+          }
+      }
+      double dsum = 0; int ne = 0;
+      for (int t : tab) if (t >= 0) { dsum += depth[t]; ++ne; }
+      std::printf("qt level %d (%dx%d): %d non-empty cells, mean start depth %.2f\n", lvl, res, res, ne, ne ? dsum / ne : 0.0);
+      g_qt_tab.push_back(tab);
+    }
+  }
   std::printf("tree: %zu nodes, depth %d, big %zu\n", S.t.nodes.size(), S.t.depth, S.t.big.size());
   Ctx C{&S, {}, 1200, spp, 50};
   const double lf[3] = {13, 2, 3}, la[3] = {0, 0, 0}, vup[3] = {0, 1, 0};
@@ -424,10 +625,15 @@ int main(int argc, char** argv) {
     h = mix32(h + 1);
     pick.push_back(int(h % uint32_t(gx * (gy - 1))));
   }
-  const char* names[] = {"wave (shipped)", "sort by octant", "sort by octant+body", "sort by visits (bound)"};
-  const int pol[] = {0, 1, 1, 1}, km[] = {0, 1, 2, 3};
+  const char* names[] = {"wave (shipped)", "sort by octant", "sort by octant+body", "sort by visits (bound)",
+                         "restart (RK lanes)", "compact (no sort)"};
+  const int pol[] = {0, 1, 1, 1, 2, 1}, km[] = {0, 1, 2, 3, 0, 4};
+  if (std::getenv("RJ")) g_charge_rej = std::atoi(std::getenv("RJ"));
+  if (std::getenv("RK")) g_restart_k = std::atoi(std::getenv("RK"));
+  const int v0 = std::getenv("V0") ? std::atoi(std::getenv("V0")) : 0;
   const int nv = std::getenv("NV") ? std::atoi(std::getenv("NV")) : 4;
-  for (int v = 0; v < nv; ++v) {
+  for (int v = v0; v < nv; ++v) {
+    if (pol[v] == 1 && std::getenv("NOSORT")) continue;
     Result R;
     g_leaf_passes = g_exact_passes = 0;
     for (int t : pick) run_tile(C, t % gx, t / gx, pol[v], km[v], R);
@@ -438,6 +644,7 @@ int main(int argc, char** argv) {
     std::printf("  rejection loops per wave-iter: disk %.2f ball %.2f (one merged loop: %.2f); absorption in %.3f of wave-iters\n",
                 g_disk / R.iters, g_ball / R.iters, g_both / R.iters, g_abs / R.iters);
     g_disk = g_ball = g_both = g_abs = 0;
+    if (g_qt) { std::printf("  qt: %.3f of segments skip the tree\n", g_qt_skip / g_qt_n); g_qt_skip = g_qt_n = 0; }
     std::printf("  candidates rejected by the t bound: %.3f of %.0f; per segment: %.2f node visits, %.2f leaves\n",
                 g_rej / g_cand, g_cand, g_visits / g_segs, g_leafs / g_segs);
     g_rej = g_cand = g_segs = g_visits = g_leafs = 0;
