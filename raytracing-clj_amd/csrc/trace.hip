@@ -475,13 +475,14 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float D = __builtin_amdgcn_sqrtf(fmaf(ecz, ecz, fmaf(ecy, ecy, ecx * ecx))) + a.bvh_r;
       const float P = fmaf(2e-3f, D, 1e-6f);
       if constexpr (STATS) st_fl += 27;   // o - c, D, P, 3 rcp, 6 slab offsets
-      // |u| >= 1e-24 keeps 1/u finite: with u = 0 an infinite 1/u makes the
-      // fma bounds NaN and -inf, which would collapse the slab (a false miss);
-      // finite, the slab of an origin inside the padded box spans ~+-1e24 and
-      // one outside it lies ~1e24 away (culled) -- the u = 0 answers.
-      const float rux = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(ux), 1e-24f), ux));
-      const float ruy = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uy), 1e-24f), uy));
-      const float ruz = __builtin_amdgcn_rcpf(copysignf(fmaxf(fabsf(uz), 1e-24f), uz));
+      // 1/u clamped to +-1e24 (one v_med3): with u = 0 an infinite 1/u makes
+      // the fma bounds NaN and -inf, which would collapse the slab (a false
+      // miss); finite, the slab of an origin inside the padded box spans
+      // ~+-1e24 and one outside it lies ~1e24 away (culled) -- the u = 0
+      // answers.  (u = -0 gives -inf -> -1e24: the sign still orders the planes.)
+      const float rux = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(ux), -1e24f, 1e24f);
+      const float ruy = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(uy), -1e24f, 1e24f);
+      const float ruz = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(uz), -1e24f, 1e24f);
       const f2 ix2 = {rux, rux}, iy2 = {ruy, ruy}, iz2 = {ruz, ruz};
       // the min plane's bound b*(1/u) - (o' + P)/u, the max plane's
       // b*(1/u) - (o' - P)/u; by the sign of 1/u one is the near plane
@@ -883,6 +884,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       } else {
         // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
         const float ri = front ? m.x : m.w;   // 1/eta (host-divided) : eta
+        const float r0 = front ? m.y : m.z;   // Schlick's r0 for that ri (host-computed, same ops)
         if constexpr (STATS) st_fl += 9;
         const float un = fmaf(uz, nz, fmaf(uy, ny, ux * nx));
         const float cosv = fminf(-un, 1.0f);
@@ -890,9 +892,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         bool refl = !(ri * sinv <= 1.0f);
         if (!refl && !a.realm) {   // (realm: no Schlick term, no draw; realm/raytracing.clj:158-177)
           const float xi = rng_uniform(st);  // drawn only when refraction is possible
-          if constexpr (STATS) st_fl += 11;
-          float r0 = (1.0f - ri) / (1.0f + ri);
-          r0 = r0 * r0;
+          if constexpr (STATS) st_fl += 8;   // xi, x1, x2, x5, 1 - r0, fma, compare (r0: host)
           const float x1 = 1.0f - cosv;
           const float x2 = x1 * x1;
           const float x5 = x2 * x2 * x1;
@@ -1302,7 +1302,18 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     sph[i] = make_float4(q[0], q[1], q[2], 1.0f / r);                   // 1/r for the normal
     const float* m = s->mat + 4 * i;
     mat[i] = make_float4(m[0], m[1], m[2], m[3]);
-    if (s->mat_kind[i] == RT_DIELECTRIC) mat[i].x = 1.0f / m[3];       // 1/eta (albedo unused)
+    if (s->mat_kind[i] == RT_DIELECTRIC) {   // (albedo unused)
+      mat[i].x = 1.0f / m[3];                // ri of a front face: 1/eta
+      // Schlick's r0 = ((1 - ri) / (1 + ri))^2 for ri = 1/eta (front face) and
+      // eta (back face): the kernel's fp32 ops, done once here (IEEE division,
+      // no contraction: the same bits)
+      for (int f = 0; f < 2; ++f) {
+        const float ri = f == 0 ? mat[i].x : m[3];
+        float r0 = (1.0f - ri) / (1.0f + ri);
+        r0 = r0 * r0;
+        (f == 0 ? mat[i].y : mat[i].z) = r0;
+      }
+    }
     kind[i] = s->mat_kind[i];
   }
   // pair-interleaved copy for the packed scan: (x0 x1 y0 y1 z0 z1 w0 w1) per pair

@@ -92,6 +92,13 @@ static float g_qt_m = 0.1f;
 static float g_qt_lo[2], g_qt_cell[2];
 static std::vector<std::vector<int>> g_qt_tab;   // per level: res_k x res_k start nodes
 static double g_qt_skip = 0, g_qt_start_depth = 0, g_qt_n = 0;
+// QT=2: one start node per wave (the wave's lanes stay in step): a probe
+// pass records each lane's segment-end cells, the wave's start is the entry
+// of the finest level whose cell holds all of them
+static bool g_probe = false;
+static int g_probe_valid = 0, g_probe_c[4];
+static int g_force_start = 0;
+static double C_QT = 30;
 
 static int g_candbit = 0;   // the body's position in its leaf (candidate bitmask)
 static void body_test(const float* s, float ox, float oy, float oz, float ux, float uy, float uz,
@@ -153,8 +160,12 @@ static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float u
       t0 = std::max(t0, std::min(a, b));
       t1 = std::min(t1, std::max(a, b));
     }
-    g_qt_n += 1;
-    if (!(t0 <= t1)) { g_qt_skip += 1; return best; }
+    if (!g_probe) g_qt_n += 1;
+    if (!(t0 <= t1)) {
+      if (g_probe) { g_probe_valid = 0; return best; }
+      g_qt_skip += 1;
+      return best;
+    }
     if (!std::isfinite(t1)) t1 = t0;   // (not reached: the box is finite)
     int c0[2], c1[2];
     const float u2[2] = {ux, uz}, e2[2] = {ex, ez};
@@ -164,9 +175,17 @@ static Hit trace(const Scene& S, float ox, float oy, float oz, float ux, float u
       c0[k] = std::clamp(int(std::floor(a)), 0, g_qt_res - 1);
       c1[k] = std::clamp(int(std::floor(b)), 0, g_qt_res - 1);
     }
+    if (g_probe) {
+      g_probe_valid = 1;
+      g_probe_c[0] = c0[0]; g_probe_c[1] = c0[1]; g_probe_c[2] = c1[0]; g_probe_c[3] = c1[1];
+      return best;
+    }
     const unsigned x = unsigned(c0[0] ^ c1[0]) | unsigned(c0[1] ^ c1[1]);
     const int lvl = x ? 32 - __builtin_clz(x) : 0;
-    if (lvl < int(g_qt_tab.size())) {
+    if (g_qt == 2) {
+      if (g_force_start == -2) { g_qt_skip += 1; return best; }
+      node = g_force_start;
+    } else if (lvl < int(g_qt_tab.size())) {
       const int res = g_qt_res >> lvl;
       const int st = g_qt_tab[lvl][(c0[1] >> lvl) * res + (c0[0] >> lvl)];
       if (st == -2) { g_qt_skip += 1; return best; }
@@ -466,6 +485,33 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
       std::vector<Trav> tr(64);
       std::vector<const Trav*> act;
       std::vector<int> done;
+      if (g_qt == 2) {   // probe pass on copies: the wave's common start node
+        int ref[2] = {-1, -1};
+        unsigned xo = 0;
+        g_probe = true;
+        for (int l = 0; l < 64; ++l) {
+          Path cp = lanes[64 * w + l];
+          if (cp.j < 0) continue;
+          int px, py;
+          pixel(cp.j, px, py);
+          Trav t;
+          g_probe_valid = 0;
+          step(C, cp, px, py, t);
+          if (!g_probe_valid) continue;
+          if (ref[0] < 0) { ref[0] = g_probe_c[0]; ref[1] = g_probe_c[1]; }
+          xo |= unsigned(g_probe_c[0] ^ ref[0]) | unsigned(g_probe_c[2] ^ ref[0]) |
+                unsigned(g_probe_c[1] ^ ref[1]) | unsigned(g_probe_c[3] ^ ref[1]);
+        }
+        g_probe = false;
+        const int lvl = xo ? 32 - __builtin_clz(xo) : 0;
+        g_force_start = 0;
+        if (ref[0] >= 0 && lvl < int(g_qt_tab.size())) {
+          const int res = g_qt_res >> lvl;
+          g_force_start = g_qt_tab[lvl][(ref[1] >> lvl) * res + (ref[0] >> lvl)];
+        }
+        wc[w] += C_QT;
+        R.cost += C_QT;
+      }
       for (int l = 0; l < 64; ++l) {
         Path& p = lanes[64 * w + l];
         if (p.j < 0) continue;
