@@ -88,6 +88,12 @@ struct alignas(16) KArgs {
   int tiles_x;               // 8 x 8 tiles per tile row
   int n_whole, split;
   int split_k0[65];          // first sample of each split (split_k0[split] = spp)
+  // n / d as the high half of n * m, m = ceil(2^64 / d) (magic64; m = 0 for
+  // d = 1: n itself), exact for every 32-bit n: the kernel divides nothing,
+  // so no division has its reciprocal set-up hoisted into loop registers
+  uint64_t cnt_magic[3];     // d = spp (whole tiles), cnt_lo, cnt_lo + 1 (splits)
+  int cnt_lo;                // spp / split
+  uint64_t rt_magic;         // d = row_tile
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
@@ -174,6 +180,11 @@ __device__ __forceinline__ uint32_t fix24(float c) {
   uint32_t r;
   asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(c * 0x1p24f));
   return r;
+}
+
+// n / d by the host's 64-bit magic m (KArgs)
+__device__ __forceinline__ int div_magic(int n, uint64_t m) {
+  return m ? static_cast<int>(__umul64hi(static_cast<uint64_t>(static_cast<uint32_t>(n)), m)) : n;
 }
 
 // stats build only: shader-clock stamp (s_memtime, drains lgkm; diagnostic)
@@ -284,7 +295,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // compacted output row -> global image row (interleaved row tiles)
   auto image_row = [&](int r) {
     if (a.tile_step > 0) {
-      const int t = r / a.row_tile;
+      const int t = div_magic(r, a.rt_magic);
       return a.row_begin + (a.tile_first + t * a.tile_step) * a.row_tile + (r - t * a.row_tile);
     }
     return a.row_begin + r;
@@ -299,10 +310,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int k0 = split ? a.split_k0[split_ix] : 0;
   const int cnt = split ? a.split_k0[split_ix + 1] - k0 : a.spp;
   // pool index j -> (pixel q = j / cnt, sample k0 + j % cnt); the next free
-  // index is `base`.  j / cnt by multiply-high: exact while j * cnt < 2^32,
-  // i.e. 64 * cnt^2 < 2^32 (cnt <= 8191; integer division above, and for
-  // cnt = 1); q / vw likewise (q < 64, vw <= 8)
-  const uint32_t cnt_magic = (cnt > 1 && cnt <= 8191) ? 0xffffffffu / static_cast<uint32_t>(cnt) + 1u : 0u;
+  // index is `base`.  j / cnt by the host's 64-bit magic; q / vw by
+  // multiply-high (exact: q < 64, vw <= 8)
+  const uint64_t cnt_magic = !split ? a.cnt_magic[0] : cnt == a.cnt_lo ? a.cnt_magic[1] : a.cnt_magic[2];
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
@@ -334,8 +344,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         }
       }
       // pool index -> (pixel, sample)
-      if (cnt_magic) q = static_cast<int>(__umulhi(static_cast<uint32_t>(j), cnt_magic));
-      else q = cnt == 1 ? j : static_cast<int>(static_cast<uint32_t>(j) / static_cast<uint32_t>(cnt));
+      q = div_magic(j, cnt_magic);
       k = j - q * cnt;
       const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
       const int px = qx0 + (q - qy * vw);
@@ -1477,6 +1486,11 @@ static int dbg_buffers(int device, unsigned long long** dbg, unsigned long long*
   return RT_OK;
 }
 
+// ceil(2^64 / d), 0 for d <= 1: n / d = the high half of n * m for every
+// 32-bit n (m * d = 2^64 + e with e < d, so n * e < 2^64 never reaches the
+// quotient)
+static uint64_t magic64(int d) { return d <= 1 ? 0 : ~0ull / static_cast<uint64_t>(d) + 1ull; }
+
 // Sample split (rt_launch): split every tile of a launch with fewer tiles
 // than kSplitRounds x (resident workgroups), into enough splits to reach that
 // (at most kSplitMax).  tools/shard_time.py on C1's 1/2/4/8-GPU shards
@@ -1604,6 +1618,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.split = split;
   a.n_whole = n_whole;
   for (int k = 0; k <= split; ++k) a.split_k0[k] = static_cast<int>(static_cast<int64_t>(k) * p->spp / split);
+  a.cnt_lo = p->spp / split;
+  a.cnt_magic[0] = magic64(p->spp);
+  a.cnt_magic[1] = magic64(a.cnt_lo);
+  a.cnt_magic[2] = magic64(a.cnt_lo + 1);
+  a.rt_magic = magic64(a.row_tile);
   const int64_t n_units64 = n_whole + static_cast<int64_t>(n_tiles - n_whole) * split;
   if (n_units64 > INT_MAX) return set_error(RT_E_ARG, "rt_launch: frame too large");
   const int n_units = static_cast<int>(n_units64);
