@@ -228,8 +228,12 @@ struct alignas(16) KNode {
 static_assert(sizeof(KNode) == 80, "KNode layout");
 
 // The pool tile: 8 x 8 pixels per 256-thread workgroup
+// The pool tile: 8 pixels wide, 8 rows high -- 4 for the 8-body-leaf
+// traversal, whose large-scene LDS image (C4: 1000 bodies) needs the 768 B
+// that half the pixel sums give back to stay at 5 workgroups per CU
 constexpr int kTile = 8;
 constexpr int kPoolPx = kTile * kTile;
+constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : kTile; }
 
 template <int SRC, int SCAN, bool STATS = false>
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
@@ -241,7 +245,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // ds_add per wave event, then an mbcnt prefix).  The colour sums are u64
   // per pixel and channel in LDS, added with ds_add_u64: order-free.
   __shared__ int s_pool_next;
-  __shared__ unsigned long long s_acc[kPoolPx * 3];
+  constexpr int TH = tile_rows(SCAN);   // tile rows
+  constexpr int NPX = kTile * TH;       // pool pixels
+  __shared__ unsigned long long s_acc[NPX * 3];
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
   if (threadIdx.x == 0) s_pool_next = 256;
-  if (threadIdx.x < kPoolPx * 3) s_acc[threadIdx.x] = 0ull;
+  if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
   if constexpr (SRC == SRC_LDS) {
     if constexpr (is_bvh_scan(SCAN)) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
@@ -287,9 +293,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int tile = a.tile_order ? a.tile_order[pos] : pos;
   const int tby = tile / a.tiles_x, tbx = tile - tby * a.tiles_x;
   // the tile's in-image part, vw x vh pixels; pool pixel q at (q % vw, q / vw)
-  const int qx0 = tbx * kTile, qy0 = tby * kTile;
+  const int qx0 = tbx * kTile, qy0 = tby * TH;
   const int vw = max(0, min(kTile, a.width - qx0));
-  const int vh = max(0, min(kTile, a.rows_out - qy0));
+  const int vh = max(0, min(TH, a.rows_out - qy0));
   const int npx = vw * vh;
 
   // compacted output row -> global image row (interleaved row tiles)
@@ -1080,15 +1086,15 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
 // per split tile, thread t = tile row * 24 + x * 3 + channel.
 __global__ __launch_bounds__(192) void finalize_kernel(const unsigned long long* __restrict__ part,
                                                         const int* __restrict__ order, int n_whole, int split,
-                                                        int tiles_x, int width, int rows, float* __restrict__ out,
-                                                        int spp, int realm) {
+                                                        int tiles_x, int tile_h, int width, int rows,
+                                                        float* __restrict__ out, int spp, int realm) {
   const int pos = n_whole + static_cast<int>(blockIdx.x);
   const int tile = order ? order[pos] : pos;
   const int tby = tile / tiles_x, tbx = tile - tby * tiles_x;
   const int t = static_cast<int>(threadIdx.x);
   const int row = t / (kTile * 3), col = t - row * (kTile * 3);
-  const int y = tby * kTile + row, x3 = tbx * kTile * 3 + col;
-  if (y >= rows || x3 >= width * 3) return;
+  const int y = tby * tile_h + row, x3 = tbx * kTile * 3 + col;
+  if (row >= tile_h || y >= rows || x3 >= width * 3) return;
   const size_t n = static_cast<size_t>(rows) * width * 3;
   const size_t e = static_cast<size_t>(y) * width * 3 + x3;
   unsigned long long sum = 0;
@@ -1119,51 +1125,52 @@ struct Variant {
   const void* fn;
   bool lds;
   bool stats;
+  int scan;   // SCAN_* (the tile shape: tile_rows)
 };
 constexpr int kVariants = 20;
 // the tree a traversal variant walks: 0 = 2-body leaves, 1 = 4, 2 = 8
 static int variant_tree(int v) { return v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 #define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
 static const Variant& variant_table(int v) {
-  static const Variant none{nullptr, false, false};
+  static const Variant none{nullptr, false, false, 0};
   static const Variant t[kVariants] = {
-      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false},          // 0: placeholder (resolved per scene)
+      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false, SCAN_BVHQ},          // 0: placeholder (resolved per scene)
 #ifdef RTCLJ_DIAG
-      {RT_K(SRC_LDS, SCAN_SIMPLE, false), true, false},        // 1
-      {RT_K(SRC_SCALAR, SCAN_SIMPLE, false), false, false},    // 2
-      {RT_K(SRC_LDS, SCAN_SIMPLE, true), true, true},          // 3
-      {RT_K(SRC_LDS, SCAN_GROUP4, false), true, false},        // 4
+      {RT_K(SRC_LDS, SCAN_SIMPLE, false), true, false, SCAN_SIMPLE},        // 1
+      {RT_K(SRC_SCALAR, SCAN_SIMPLE, false), false, false, SCAN_SIMPLE},    // 2
+      {RT_K(SRC_LDS, SCAN_SIMPLE, true), true, true, SCAN_SIMPLE},          // 3
+      {RT_K(SRC_LDS, SCAN_GROUP4, false), true, false, SCAN_GROUP4},        // 4
 #else
       none, none, none, none,
 #endif
-      {RT_K(SRC_SCALAR, SCAN_GROUP4, false), false, false},    // 5
+      {RT_K(SRC_SCALAR, SCAN_GROUP4, false), false, false, SCAN_GROUP4},    // 5
 #ifdef RTCLJ_DIAG
-      {RT_K(SRC_LDS, SCAN_GROUP4, true), true, true},          // 6
-      {RT_K(SRC_SCALAR, SCAN_GROUP4, true), false, true},      // 7
-      {RT_K(SRC_LDS, SCAN_PK4, false), true, false},           // 8
-      {RT_K(SRC_SCALAR, SCAN_PK4, false), false, false},       // 9
-      {RT_K(SRC_SCALAR, SCAN_PK4, true), false, true},         // 10
-      {RT_K(SRC_LDS, SCAN_BVH, false), true, false},           // 11
+      {RT_K(SRC_LDS, SCAN_GROUP4, true), true, true, SCAN_GROUP4},          // 6
+      {RT_K(SRC_SCALAR, SCAN_GROUP4, true), false, true, SCAN_GROUP4},      // 7
+      {RT_K(SRC_LDS, SCAN_PK4, false), true, false, SCAN_PK4},           // 8
+      {RT_K(SRC_SCALAR, SCAN_PK4, false), false, false, SCAN_PK4},       // 9
+      {RT_K(SRC_SCALAR, SCAN_PK4, true), false, true, SCAN_PK4},         // 10
+      {RT_K(SRC_LDS, SCAN_BVH, false), true, false, SCAN_BVH},           // 11
 #else
       none, none, none, none, none, none,
 #endif
-      {RT_K(SRC_SCALAR, SCAN_BVH, false), false, false},       // 12
+      {RT_K(SRC_SCALAR, SCAN_BVH, false), false, false, SCAN_BVH},       // 12
 #ifdef RTCLJ_DIAG
-      {RT_K(SRC_LDS, SCAN_BVH, true), true, true},             // 13
-      {RT_K(SRC_LDS, SCAN_BVHWW, false), true, false},         // 14
-      {RT_K(SRC_LDS, SCAN_BVHWW, true), true, true},           // 15
+      {RT_K(SRC_LDS, SCAN_BVH, true), true, true, SCAN_BVH},             // 13
+      {RT_K(SRC_LDS, SCAN_BVHWW, false), true, false, SCAN_BVHWW},         // 14
+      {RT_K(SRC_LDS, SCAN_BVHWW, true), true, true, SCAN_BVHWW},           // 15
 #else
       none, none, none,
 #endif
-      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false},          // 16
+      {RT_K(SRC_LDS, SCAN_BVHQ, false), true, false, SCAN_BVHQ},          // 16
 #ifdef RTCLJ_DIAG
-      {RT_K(SRC_LDS, SCAN_BVHQ, true), true, true},            // 17
+      {RT_K(SRC_LDS, SCAN_BVHQ, true), true, true, SCAN_BVHQ},            // 17
 #else
       none,
 #endif
-      {RT_K(SRC_LDS, SCAN_BVHO, false), true, false},          // 18
+      {RT_K(SRC_LDS, SCAN_BVHO, false), true, false, SCAN_BVHO},          // 18
 #ifdef RTCLJ_DIAG
-      {RT_K(SRC_LDS, SCAN_BVHO, true), true, true},            // 19
+      {RT_K(SRC_LDS, SCAN_BVHO, true), true, true, SCAN_BVHO},            // 19
 #else
       none,
 #endif
@@ -1413,7 +1420,7 @@ static size_t stack_of(const DTree& t, int tree) {
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the kernel's
 // static LDS (pool counter + the 64 pixels' colour sums)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;   // (the 8-body traversal's 8x4 tile: 768 B less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
@@ -1571,7 +1578,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  const int gx = (p->width + kTile - 1) / kTile, gy = (rows + kTile - 1) / kTile;
+  const int th = tile_rows(v.scan);   // the variant's tile rows
+  const int gx = (p->width + kTile - 1) / kTile, gy = (rows + th - 1) / th;
   const dim3 block(256);
   const int n_tiles = gx * gy;
   a.tiles_x = gx;
@@ -1676,9 +1684,9 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   if (split > 1) {
     const unsigned long long* part = a.part;
     const int* order = a.tile_order;
-    int nw = n_whole, sp = split, tx = gx, w = p->width, nr = rows, spp = p->spp, realm = a.realm;
+    int nw = n_whole, sp = split, tx = gx, tht = th, w = p->width, nr = rows, spp = p->spp, realm = a.realm;
     float* out = d_out;
-    void* fargs[] = {&part, &order, &nw, &sp, &tx, &w, &nr, &out, &spp, &realm};
+    void* fargs[] = {&part, &order, &nw, &sp, &tx, &tht, &w, &nr, &out, &spp, &realm};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&finalize_kernel), dim3(n_tiles - n_whole), dim3(192),
                             fargs, 0, stream));
   }
