@@ -382,11 +382,16 @@ def main():
         step()
         ends[k].record(stream)
     torch.cuda.synchronize()
+    # each rank's own steps, from the common barrier to its last kernel's end;
+    # the max over ranks below is the job's time (the closing barrier itself,
+    # a host round trip of every rank, is not render time: elapsed_barrier_s)
+    t1 = time.perf_counter()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = t1 - t0
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     cnt = counters.to("cpu").tolist()
-    mine = {"rank": rank, "device": device, "elapsed_s": elapsed, "kernel_ms_avg": sum(kern_ms) / len(kern_ms),
+    mine = {"rank": rank, "device": device, "elapsed_s": elapsed, "elapsed_barrier_s": time.perf_counter() - t0,
+            "kernel_ms_avg": sum(kern_ms) / len(kern_ms),
             "kernel_ms_max": max(kern_ms), "rows": rows, "segments": cnt[0], "samples": cnt[1]}
     per_rank = [mine]
     if world > 1:
@@ -455,7 +460,9 @@ def main():
             "valu": valu, "occupancy": occ, "stats_build": stats,
             "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": mine["kernel_ms_max"],
             "per_rank": {"kernel_ms_avg": kms, "rows": [r["rows"] for r in per_rank],
-                         "imbalance": max(kms) / (sum(kms) / len(kms))},
+                         "imbalance": max(kms) / (sum(kms) / len(kms)),
+                         "elapsed_ms": [r["elapsed_s"] * 1e3 for r in per_rank],
+                         "elapsed_with_closing_barrier_ms": max(r["elapsed_barrier_s"] for r in per_rank) * 1e3},
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_total / a.steps,
             "kernel": "rtclj::trace_kernel<SRC,SCAN,STATS> (default: BVH with 4-body leaves in LDS, 8x8-pixel "
                       "sample pool per 256-thread workgroup, fixed-point colour sums in LDS)",
