@@ -275,7 +275,9 @@ int rt_set_schedule(int mode);
  * Synchronises the devices. */
 int rt_debug_stats(uint64_t* out32);
 
-/* Diagnostic wave timeline of the stats variants' last launches on `device`:
+/* Diagnostic wave timeline of the stats variants' last launches on `device`
+ * (of every variant's when the diagnostic build is loaded with
+ * RTCLJ_TIMELINE=1):
  * n_waves x {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID}; returns
  * the count. */
 int rt_debug_waves(int device, uint64_t* out, size_t n_waves);

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   uint64_t st_fresh = 0, st_fresh_lanes = 0;  // wave-level camera-sample blocks, lanes in them
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
-  if (STATS || a.tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
+  if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
   if (threadIdx.x == 0) s_pool_next = 256;
@@ -1032,14 +1032,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       atomicAdd(&a.dbg[10], static_cast<unsigned long long>(c2));
       atomicAdd(&a.dbg[11], static_cast<unsigned long long>(c3));
     }
-    if (a.dbgw && lane == 0) {
-      const size_t wid = static_cast<size_t>(slot) * 4 + (threadIdx.x >> 6);   // by dispatch slot
-      if (wid < 65536) {
-        a.dbgw[4 * wid + 0] = st_t0;
-        a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-        a.dbgw[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-        a.dbgw[4 * wid + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
-      }
+  }
+  // wave timeline (stats variants, or any variant under RTCLJ_TIMELINE in
+  // the diagnostic build; NULL otherwise: a uniform branch)
+  if (a.dbgw && lane == 0) {
+    const size_t wid = static_cast<size_t>(slot) * 4 + (threadIdx.x >> 6);   // by dispatch slot
+    if (wid < 65536) {
+      a.dbgw[4 * wid + 0] = st_t0;
+      a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+      a.dbgw[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      a.dbgw[4 * wid + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
     }
   }
   if (a.counters) {
@@ -1187,6 +1189,13 @@ static const bool g_bvh_sah = [] {
   const char* e = std::getenv("RTCLJ_BVH");
   return !(e && std::strcmp(e, "median") == 0);
 }();
+#ifdef RTCLJ_DIAG
+// diagnostic build: RTCLJ_TIMELINE=1 records every launch's wave timeline
+static const bool g_timeline = [] {
+  const char* e = std::getenv("RTCLJ_TIMELINE");
+  return e && std::atoi(e) != 0;
+}();
+#endif
 // stats builds: per device, u64[kDbg] event counters and the u64[4 * 65536]
 // wave timeline, allocated on that device at its first stats launch
 constexpr int kDbg = 32;
@@ -1587,6 +1596,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     const int rc = dbg_buffers(ds->device, &a.dbg, &a.dbgw);
     if (rc != RT_OK) return rc;
   }
+#ifdef RTCLJ_DIAG
+  else if (g_timeline) {   // wave timeline only (rt_debug_waves), no counters
+    unsigned long long* unused = nullptr;
+    const int rc = dbg_buffers(ds->device, &unused, &a.dbgw);
+    if (rc != RT_OK) return rc;
+  }
+#endif
   const size_t lds = launch_lds(*ds, vsel);
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
