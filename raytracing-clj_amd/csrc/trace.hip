@@ -321,6 +321,22 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const uint64_t cnt_magic = !split ? a.cnt_magic[0] : cnt == a.cnt_lo ? a.cnt_magic[1] : a.cnt_magic[2];
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
+  // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
+  // key and coordinates, so a camera sample costs one LDS read instead of
+  // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
+  // image has no room for it: C4 keeps 5 workgroups per CU)
+  constexpr bool kPixelTable = SCAN == SCAN_BVHQ;
+  __shared__ float4 s_px[kPixelTable ? NPX : 1];
+  if constexpr (kPixelTable) {
+    const int t = static_cast<int>(threadIdx.x);
+    if (t < npx) {
+      const int qy = vw == 1 ? t : static_cast<int>(__umulhi(static_cast<uint32_t>(t), mag_vw));
+      const int px = qx0 + (t - qy * vw);
+      const int gy = image_row(qy0 + qy);
+      s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
+    }
+    __syncthreads();
+  }
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
   bool active = j < pool;
 
@@ -352,15 +368,27 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // pool index -> (pixel, sample)
       q = div_magic(j, cnt_magic);
       k = j - q * cnt;
-      const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
-      const int px = qx0 + (q - qy * vw);
-      const int gy = image_row(qy0 + qy);
+      uint32_t pk;
+      float fpx, fgy;
+      if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
+        const float4 pt = s_px[q];
+        pk = __float_as_uint(pt.x);
+        fpx = pt.y;
+        fgy = pt.z;
+      } else {
+        const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
+        const int px = qx0 + (q - qy * vw);
+        const int gy = image_row(qy0 + qy);
+        pk = pixel_key(px, gy);
+        fpx = static_cast<float>(px);
+        fgy = static_cast<float>(gy);
+      }
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
-      st = mix32(pixel_key(px, gy) + static_cast<uint32_t>(a.sample_begin + k0 + k) * 0x9e3779b9u);
+      st = mix32(pk + static_cast<uint32_t>(a.sample_begin + k0 + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
       // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
-      const float fx = static_cast<float>(px) + rng_centered(st);
-      const float fy = static_cast<float>(gy) + rng_centered(st);
+      const float fx = fpx + rng_centered(st);
+      const float fy = fgy + rng_centered(st);
       const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
       const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
@@ -1427,9 +1455,10 @@ static size_t stack_of(const DTree& t, int tree) {
   return static_cast<size_t>(t.depth + 2) * 256 * (tree == 2 ? 1 : 2);
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
-// LDS a CU can give each of 5 workgroups (160 KB / 5), less the kernel's
-// static LDS (pool counter + the 64 pixels' colour sums)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;   // (the 8-body traversal's 8x4 tile: 768 B less)
+// LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
+// kernel's static LDS (pool counter, the 64 pixels' colour sums and their
+// pixel table)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal's 8x4 tile, no table: 1.8 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
