@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--row-tile", type=int, default=8, help="rows per interleaved shard tile")
     ap.add_argument("--configs", nargs="*", default=[""],
                     help="environment settings per measurement, e.g. RTCLJ_SPLIT=4,RTCLJ_RING=2 ('' = defaults)")
     a = ap.parse_args()
@@ -67,7 +68,7 @@ def run(a, wl, W, H, spp, sc, cam, sh, stream):
         for r in range(n):
             ds = C.c_void_p()
             check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
-            p = rt_params(**shard_params(n, r, W, H, spp, wl["depth"], 1, "strong"))
+            p = rt_params(**shard_params(n, r, W, H, spp, wl["depth"], 1, "strong", row_tile=a.row_tile))
             rows = check(lib.rt_rows_out(C.byref(p)))
             out = torch.empty(rows * W * 3, dtype=torch.float32, device="cuda")
             cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
