@@ -204,7 +204,10 @@ def stats_leg(scene, cam, p, device, out_numel):
     res = {"stats_variant": sv, "flops_per_segment": dbg[18] / segs, "segments_per_sample": segs / smp,
            "per_wave_iter": {"wave_iters_per_sample": wi / smp, "lanes_active": dbg[1] / wi / 64.0,
                              "fresh_blocks": dbg[16] / wi, "fresh_lanes": dbg[17] / max(dbg[16], 1),
-                             "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi}}
+                             "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi,
+                             "dielectric_blocks": dbg[19] / wi, "dielectric_lanes": dbg[20] / max(dbg[19], 1),
+                             "lambert_metal_blocks": dbg[21] / wi,
+                             "lambert_metal_lanes": dbg[22] / max(dbg[21], 1)}}
     if v != 5:
         res.update({"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs,
                     "exact_tests": dbg[4] / segs})

@@ -271,7 +271,9 @@ int rt_set_schedule(int mode);
  * wave-level leaf passes, [13] wave-level exact-test passes, [14] / [15]
  * wave-level trips of the random-unit-vec3 / defocus-disk rejection loops,
  * [16] / [17] wave-level camera-sample blocks / lanes in them, [18] executed
- * fp32 flops (per lane, fma = 2), [19..31] 0.
+ * fp32 flops (per lane, fma = 2), [19] / [20] wave-level
+ * dielectric shading blocks / lanes in them, [21] / [22] wave-level
+ * lambertian-or-metal shading blocks / lanes in them, [23..31] 0.
  * Synchronises the devices. */
 int rt_debug_stats(uint64_t* out32);
 

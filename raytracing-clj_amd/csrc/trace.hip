@@ -254,6 +254,8 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   uint64_t st_ball = 0, st_disk = 0;          // wave-level rejection-loop trips (random-unit, disk)
   uint64_t st_fl = 0;                         // executed fp32 flops of this lane (fma = 2)
   uint64_t st_fresh = 0, st_fresh_lanes = 0;  // wave-level camera-sample blocks, lanes in them
+  uint64_t st_diel = 0, st_diel_lanes = 0;    // wave-level dielectric blocks, lanes in them
+  uint64_t st_lm = 0, st_lm_lanes = 0;        // wave-level lambertian/metal blocks, lanes in them
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
@@ -885,6 +887,13 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       oz = hz;
       last = best;
       if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
+        if constexpr (STATS) {
+          const uint64_t ex = __builtin_amdgcn_read_exec();
+          if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+            ++st_lm;
+            st_lm_lanes += __popcll(ex);
+          }
+        }
         // one random-unit-vec3 draw for either material (the only draws of
         // the segment for these lanes): a wave loops the rejection sampler
         // once for both kinds
@@ -926,6 +935,13 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         done = true;  // no ::scatter-fn -> black (raytracing.clj:49-54)
       } else {
         // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
+        if constexpr (STATS) {
+          const uint64_t ex = __builtin_amdgcn_read_exec();
+          if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
+            ++st_diel;
+            st_diel_lanes += __popcll(ex);
+          }
+        }
         const float ri = front ? m.x : m.w;   // 1/eta (host-divided) : eta
         const float r0 = front ? m.y : m.z;   // Schlick's r0 for that ri (host-computed, same ops)
         if constexpr (STATS) st_fl += 9;
@@ -1032,6 +1048,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     if (a.dbg && (st_ball | st_disk)) {
       atomicAdd(&a.dbg[14], static_cast<unsigned long long>(st_ball));
       atomicAdd(&a.dbg[15], static_cast<unsigned long long>(st_disk));
+    }
+    if (a.dbg && (st_diel | st_lm)) {
+      atomicAdd(&a.dbg[19], static_cast<unsigned long long>(st_diel));
+      atomicAdd(&a.dbg[20], static_cast<unsigned long long>(st_diel_lanes));
+      atomicAdd(&a.dbg[21], static_cast<unsigned long long>(st_lm));
+      atomicAdd(&a.dbg[22], static_cast<unsigned long long>(st_lm_lanes));
     }
     if (a.dbg && st_fresh) {
       atomicAdd(&a.dbg[16], static_cast<unsigned long long>(st_fresh));
