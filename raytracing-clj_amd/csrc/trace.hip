@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if (threadIdx.x == 0) s_pool_next = 256;
+  if (threadIdx.x == 0) s_pool_next = (SCAN == SCAN_BVHQ && !STATS) ? 0 : 256;   // (the ring claims its own)
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
   if constexpr (SRC == SRC_LDS) {
     if constexpr (is_bvh_scan(SCAN)) {
@@ -327,7 +327,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
   // image has no room for it: C4 keeps 5 workgroups per CU)
-  constexpr bool kPixelTable = SCAN == SCAN_BVHQ;
+  // (the ring below takes the pixel arithmetic out of the loop altogether:
+  // only the statistics build of this traversal keeps the table)
+  constexpr bool kRing = SCAN == SCAN_BVHQ && !STATS;
+  constexpr bool kPixelTable = SCAN == SCAN_BVHQ && !kRing;
   __shared__ float4 s_px[kPixelTable ? NPX : 1];
   if constexpr (kPixelTable) {
     const int t = static_cast<int>(threadIdx.x);
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     __syncthreads();
   }
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
-  bool active = j < pool;
+  bool active = kRing ? true : j < pool;
 
   // path state
   uint32_t st = 0;
@@ -348,7 +351,127 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   float tr = 1, tg = 1, tb = 1;
   int rem = 0;
   int last = -1;   // body the current ray leaves (-1: camera ray)
-  bool fresh = true;
+  bool fresh = !kRing;
+
+  // ---- camera-sample ring (4-body-leaf traversal) ----
+  // Each wave keeps up to 64 camera samples ready in LDS ([field][slot]: RNG
+  // state after the sample's draws, fx, fy, the disk draws' 24-bit integers
+  // with the pool pixel in the top byte of the first).  A wave whose lanes
+  // need more samples than it holds makes a batch with all its lanes at once
+  // (pool index -> pixel, two hashes, the jitter and the defocus-disk
+  // rejection loop), so that work runs with full waves instead of with the
+  // ~26 lanes that end a path in an iteration; a lane whose path ended takes
+  // the next sample from the ring and sets up its camera ray.  Every sample
+  // is computed with the same ops as before: the same bits.
+  constexpr int kRingN = 64;
+  __shared__ uint32_t s_ring[kRing ? 4 * 5 * kRingN : 1];
+  uint32_t* const ring = s_ring + (kRing ? (threadIdx.x >> 6) * 5 * kRingN : 0);
+  int r_head = 0, r_count = 0;   // wave-uniform: the next slot to hand out, samples held
+  auto ring_fill = [&](int need) {   // run by every lane still in the loop (wave-uniform branch)
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    const int nact = __popcll(ex);
+    const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(ex >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ex), 0u)));
+    // a full batch, except near the pool's end: then only what is needed now,
+    // so that no wave holds samples the workgroup's other waves could run
+    const int left = pool - __builtin_amdgcn_readfirstlane(s_pool_next);
+    const int g = left < 4 * kRingN ? need : min(kRingN - r_count, nact);
+    const int leader = __ffsll(static_cast<long long>(ex)) - 1;
+    int b = 0;
+    if (lane == leader) b = atomicAdd(&s_pool_next, g);
+    b = __builtin_amdgcn_readlane(b, leader);
+    if (rank < g) {
+      const int jj = b + rank;
+      uint32_t e_st = 0, e_a = 0xff000000u, e_b = 0;   // pixel 0xff: the pool is empty
+      float e_fx = 0.0f, e_fy = 0.0f;
+      if (jj < pool) {
+        const int qq = div_magic(jj, cnt_magic);
+        const int kk = jj - qq * cnt;
+        const int qy = vw == 1 ? qq : static_cast<int>(__umulhi(static_cast<uint32_t>(qq), mag_vw));
+        const int px = qx0 + (qq - qy * vw);
+        const int gy = image_row(qy0 + qy);
+        // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
+        uint32_t rs = mix32(pixel_key(px, gy) + static_cast<uint32_t>(a.sample_begin + k0 + kk) * 0x9e3779b9u);
+        if (rs == 0) rs = 0x6d2b79f5u;
+        e_fx = static_cast<float>(px) + rng_centered(rs);
+        e_fy = static_cast<float>(gy) + rng_centered(rs);
+        uint32_t ix = 0, iy = 0;
+        if (a.defocus) {
+          // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86):
+          // rng_sym's draws, kept as their 24-bit integers
+          float qx, qy2;
+          do {
+            rs ^= rs << 13;
+            rs ^= rs >> 17;
+            rs ^= rs << 5;
+            ix = rs >> 8;
+            rs ^= rs << 13;
+            rs ^= rs >> 17;
+            rs ^= rs << 5;
+            iy = rs >> 8;
+            qx = fmaf(static_cast<float>(ix), 0x1p-23f, -1.0f);
+            qy2 = fmaf(static_cast<float>(iy), 0x1p-23f, -1.0f);
+          } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        }
+        e_st = rs;
+        e_a = ix | (static_cast<uint32_t>(qq) << 24);
+        e_b = iy;
+      }
+      const int slot = (r_head + r_count + rank) & (kRingN - 1);
+      ring[0 * kRingN + slot] = e_st;
+      ring[1 * kRingN + slot] = __float_as_uint(e_fx);
+      ring[2 * kRingN + slot] = __float_as_uint(e_fy);
+      ring[3 * kRingN + slot] = e_a;
+      ring[4 * kRingN + slot] = e_b;
+    }
+    r_count += g;
+  };
+  // the lanes in `m` (wave-uniform mask, taken: lanes with take) start their
+  // next sample from the ring; a lane given no sample retires
+  auto ring_take = [&](uint64_t m, bool take) {
+    const int nt = __popcll(m);
+    if (r_count < nt) ring_fill(nt - r_count);
+    asm volatile("" ::: "memory");   // the batch's LDS writes before the reads (in order per wave)
+    if (take) {
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+      const int slot = (r_head + rank) & (kRingN - 1);
+      const uint32_t ea = ring[3 * kRingN + slot];
+      if ((ea >> 24) == 0xffu) {
+        active = false;
+      } else {
+        st = ring[0 * kRingN + slot];
+        const float fx = __uint_as_float(ring[1 * kRingN + slot]);
+        const float fy = __uint_as_float(ring[2 * kRingN + slot]);
+        q = static_cast<int>(ea >> 24);
+        const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
+        const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
+        const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
+        if (a.defocus) {
+          const float qx = fmaf(static_cast<float>(ea & 0xffffffu), 0x1p-23f, -1.0f);
+          const float qy2 = fmaf(static_cast<float>(ring[4 * kRingN + slot]), 0x1p-23f, -1.0f);
+          ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
+          oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
+          oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
+        } else {
+          ox = cx;
+          oy = cy;
+          oz = cz;
+        }
+        dx = sx - ox;
+        dy = sy - oy;
+        dz = sz - oz;
+        tr = tg = tb = 1.0f;
+        rem = a.max_depth;
+        last = -1;
+      }
+    }
+    r_head += nt;
+    r_count -= nt;
+  };
+  if constexpr (kRing) {
+    ring_take(__ballot(1), true);   // every lane's first sample
+  }
 
   while (active) {
     if constexpr (STATS) st_ts = stamp();
@@ -992,13 +1115,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     }
     // refill: one LDS atomic per wave event hands out the next popc(m) indices
     const uint64_t m = __ballot(done);
-    if (m) {
+    if constexpr (kRing) {
+      if (m) ring_take(m, done);
+    } else if (m) {
       const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
       int old = 0;
       if (lane == leader) old = atomicAdd(&s_pool_next, static_cast<int>(__popcll(m)));
       base = __builtin_amdgcn_readlane(old, leader);
     }
-    if (done) {
+    if (!kRing && done) {
       j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
       fresh = true;
@@ -1478,9 +1603,9 @@ static size_t stack_of(const DTree& t, int tree) {
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
-// kernel's static LDS (pool counter, the 64 pixels' colour sums and their
-// pixel table)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal's 8x4 tile, no table: 1.8 KB less)
+// kernel's static LDS (pool counter, the 64 pixels' colour sums and the four
+// waves' camera-sample rings)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 4 * 5 * 64 * 4 + 12;   // (the 8-body traversal's 8x4 tile, no ring: 5.9 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
