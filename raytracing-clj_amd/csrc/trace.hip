@@ -436,35 +436,36 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
       const int slot = (r_head + rank) & (kRingN - 1);
-      const uint32_t ea = ring[3 * kRingN + slot];
-      if ((ea >> 24) == 0xffu) {
-        active = false;
+      // all five fields in flight at once: the ray is set up unconditionally
+      // (from the empty entry's zeros when the pool is done: harmless, the
+      // lane retires before it traces)
+      const uint32_t e0 = ring[0 * kRingN + slot], e1 = ring[1 * kRingN + slot], e2 = ring[2 * kRingN + slot];
+      const uint32_t ea = ring[3 * kRingN + slot], eb = ring[4 * kRingN + slot];
+      st = e0;
+      const float fx = __uint_as_float(e1);
+      const float fy = __uint_as_float(e2);
+      q = static_cast<int>(ea >> 24);
+      const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
+      const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
+      const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
+      if (a.defocus) {
+        const float qx = fmaf(static_cast<float>(ea & 0xffffffu), 0x1p-23f, -1.0f);
+        const float qy2 = fmaf(static_cast<float>(eb), 0x1p-23f, -1.0f);
+        ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
+        oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
+        oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
       } else {
-        st = ring[0 * kRingN + slot];
-        const float fx = __uint_as_float(ring[1 * kRingN + slot]);
-        const float fy = __uint_as_float(ring[2 * kRingN + slot]);
-        q = static_cast<int>(ea >> 24);
-        const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
-        const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
-        const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
-        if (a.defocus) {
-          const float qx = fmaf(static_cast<float>(ea & 0xffffffu), 0x1p-23f, -1.0f);
-          const float qy2 = fmaf(static_cast<float>(ring[4 * kRingN + slot]), 0x1p-23f, -1.0f);
-          ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
-          oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
-          oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
-        } else {
-          ox = cx;
-          oy = cy;
-          oz = cz;
-        }
-        dx = sx - ox;
-        dy = sy - oy;
-        dz = sz - oz;
-        tr = tg = tb = 1.0f;
-        rem = a.max_depth;
-        last = -1;
+        ox = cx;
+        oy = cy;
+        oz = cz;
       }
+      dx = sx - ox;
+      dy = sy - oy;
+      dz = sz - oz;
+      tr = tg = tb = 1.0f;
+      rem = a.max_depth;
+      last = -1;
+      if (q == 0xff) active = false;   // the pool is done
     }
     r_head += nt;
     r_count -= nt;
