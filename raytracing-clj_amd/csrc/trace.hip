@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   __shared__ uint32_t s_ring[kRing ? 4 * 5 * kRingN : 1];
   uint32_t* const ring = s_ring + (kRing ? (threadIdx.x >> 6) * 5 * kRingN : 0);
   int r_head = 0, r_count = 0;   // wave-uniform: the next slot to hand out, samples held
+  int r_seen = 0;                // wave-uniform: the pool counter after this wave's last batch
   auto ring_fill = [&](int need) {   // run by every lane still in the loop (wave-uniform branch)
     const uint64_t ex = __builtin_amdgcn_read_exec();
     const int nact = __popcll(ex);
@@ -374,12 +375,13 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
                                                                 __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ex), 0u)));
     // a full batch, except near the pool's end: then only what is needed now,
     // so that no wave holds samples the workgroup's other waves could run
-    const int left = pool - __builtin_amdgcn_readfirstlane(s_pool_next);
-    const int g = left < 4 * kRingN ? need : min(kRingN - r_count, nact);
+    // (the pool's progress as this wave last saw it: no extra LDS read)
+    const int g = pool - r_seen < 4 * kRingN ? need : min(kRingN - r_count, nact);
     const int leader = __ffsll(static_cast<long long>(ex)) - 1;
     int b = 0;
     if (lane == leader) b = atomicAdd(&s_pool_next, g);
     b = __builtin_amdgcn_readlane(b, leader);
+    r_seen = b + g;
     if (rank < g) {
       const int jj = b + rank;
       uint32_t e_st = 0, e_a = 0xff000000u, e_b = 0;   // pixel 0xff: the pool is empty
