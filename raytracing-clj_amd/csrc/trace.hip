@@ -323,6 +323,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const uint64_t cnt_magic = !split ? a.cnt_magic[0] : cnt == a.cnt_lo ? a.cnt_magic[1] : a.cnt_magic[2];
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
+  const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;   // (the ring's order)
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
@@ -387,8 +388,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       uint32_t e_st = 0, e_a = 0xff000000u, e_b = 0;   // pixel 0xff: the pool is empty
       float e_fx = 0.0f, e_fy = 0.0f;
       if (jj < pool) {
-        const int qq = div_magic(jj, cnt_magic);
-        const int kk = jj - qq * cnt;
+        // sample-major here (pixel jj mod npx, sample jj / npx): a batch is
+        // one sample of each of the tile's pixels, neighbouring rays, and the
+        // lanes ending paths together add into different pixels' sums (the
+        // ring-less path keeps pixel-major: consecutive samples of a pixel)
+        const int kk = div_magic(jj, npx_magic);
+        const int qq = jj - kk * npx;
         const int qy = vw == 1 ? qq : static_cast<int>(__umulhi(static_cast<uint32_t>(qq), mag_vw));
         const int px = qx0 + (qq - qy * vw);
         const int gy = image_row(qy0 + qy);
