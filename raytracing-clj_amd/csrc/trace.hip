@@ -89,10 +89,9 @@ struct alignas(16) KArgs {
   int n_whole, split;
   int split_k0[65];          // first sample of each split (split_k0[split] = spp)
   // n / d as the high half of n * m, m = ceil(2^64 / d) (magic64; m = 0 for
-  // d = 1: n itself), exact for every 32-bit n: the kernel divides nothing,
-  // so no division has its reciprocal set-up hoisted into loop registers
-  uint64_t cnt_magic[3];     // d = spp (whole tiles), cnt_lo, cnt_lo + 1 (splits)
-  int cnt_lo;                // spp / split
+  // d = 1: n itself), exact for every 32-bit n: the kernel's loop divides
+  // nothing, so no division has its reciprocal set-up hoisted into loop
+  // registers (the pool's j / npx magic is made once per workgroup)
   uint64_t rt_magic;         // d = row_tile
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
@@ -317,13 +316,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // the unit's samples [k0, k0 + cnt) of each pixel
   const int k0 = split ? a.split_k0[split_ix] : 0;
   const int cnt = split ? a.split_k0[split_ix + 1] - k0 : a.spp;
-  // pool index j -> (pixel q = j / cnt, sample k0 + j % cnt); the next free
-  // index is `base`.  j / cnt by the host's 64-bit magic; q / vw by
-  // multiply-high (exact: q < 64, vw <= 8)
-  const uint64_t cnt_magic = !split ? a.cnt_magic[0] : cnt == a.cnt_lo ? a.cnt_magic[1] : a.cnt_magic[2];
+  // pool index j -> (pixel q = j % npx, sample k0 + j / npx); the next free
+  // index is `base`.  j / npx by a 64-bit magic (exact for every 32-bit j);
+  // q / vw by multiply-high (exact: q < 64, vw <= 8)
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
-  const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;   // (the ring's order)
+  const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
@@ -498,9 +496,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           st_fresh_lanes += __popcll(ex);
         }
       }
-      // pool index -> (pixel, sample)
-      q = div_magic(j, cnt_magic);
-      k = j - q * cnt;
+      // pool index -> (pixel, sample), sample-major as the ring's batches:
+      // the lanes ending paths together add into different pixels' sums
+      k = div_magic(j, npx_magic);
+      q = j - k * npx;
       uint32_t pk;
       float fpx, fgy;
       if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
@@ -1826,10 +1825,6 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.split = split;
   a.n_whole = n_whole;
   for (int k = 0; k <= split; ++k) a.split_k0[k] = static_cast<int>(static_cast<int64_t>(k) * p->spp / split);
-  a.cnt_lo = p->spp / split;
-  a.cnt_magic[0] = magic64(p->spp);
-  a.cnt_magic[1] = magic64(a.cnt_lo);
-  a.cnt_magic[2] = magic64(a.cnt_lo + 1);
   a.rt_magic = magic64(a.row_tile);
   const int64_t n_units64 = n_whole + static_cast<int64_t>(n_tiles - n_whole) * split;
   if (n_units64 > INT_MAX) return set_error(RT_E_ARG, "rt_launch: frame too large");
