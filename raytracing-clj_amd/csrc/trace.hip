@@ -386,10 +386,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       uint32_t e_st = 0, e_a = 0xff000000u, e_b = 0;   // pixel 0xff: the pool is empty
       float e_fx = 0.0f, e_fy = 0.0f;
       if (jj < pool) {
-        // sample-major here (pixel jj mod npx, sample jj / npx): a batch is
-        // one sample of each of the tile's pixels, neighbouring rays, and the
-        // lanes ending paths together add into different pixels' sums (the
-        // ring-less path keeps pixel-major: consecutive samples of a pixel)
+        // sample-major (pixel jj mod npx, sample jj / npx): a batch is one
+        // sample of each of the tile's pixels, neighbouring rays, and the
+        // lanes ending paths together add into different pixels' sums
         const int kk = div_magic(jj, npx_magic);
         const int qq = jj - kk * npx;
         const int qy = vw == 1 ? qq : static_cast<int>(__umulhi(static_cast<uint32_t>(qq), mag_vw));
