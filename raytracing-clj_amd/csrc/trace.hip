@@ -234,16 +234,33 @@ constexpr int kTile = 8;
 constexpr int kPoolPx = kTile * kTile;
 constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : kTile; }
 
+// A/B builds only ("six waves per SIMD"): -DRTCLJ_AB_WAVES6
+// caps the registers at 80 (6 waves per SIMD, with spills); -DRTCLJ_AB_NO_RING
+// makes camera samples in the loop without the pixel table, so that the
+// default traversal's LDS image fits 6 workgroups per CU
 template <int SRC, int SCAN, bool STATS = false>
+#ifdef RTCLJ_AB_WAVES6
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void trace_kernel(const KArgs a) {
+#else
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
+#endif
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
-  // indices j in [0, npx * spp), pixel-major (j -> pixel j / spp, sample
-  // j % spp: the lanes in flight hold consecutive samples of a few pixels,
-  // the most coherent rays a workgroup can hold).  Lanes start on j = 0..255;
-  // a lane whose path ends takes the next index from an LDS counter (one
-  // ds_add per wave event, then an mbcnt prefix).  The colour sums are u64
-  // per pixel and channel in LDS, added with ds_add_u64: order-free.
+  // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample
+  // j / npx: the lanes ending paths together add into different pixels'
+  // sums).  Camera samples come from per-wave rings in LDS (default
+  // traversal) or, in the other traversals, a lane whose path ends takes the
+  // next index from an LDS counter (one ds_add per wave event, then an mbcnt
+  // prefix).  The colour sums are u64 per pixel and channel in LDS, added
+  // with ds_add_u64: order-free.
   __shared__ int s_pool_next;
+  // camera samples from per-wave rings in LDS (below), for the default
+  // traversal; the other traversals and the statistics build make them in
+  // the loop
+#ifdef RTCLJ_AB_NO_RING
+  constexpr bool kRing = false;
+#else
+  constexpr bool kRing = SCAN == SCAN_BVHQ && !STATS;
+#endif
   constexpr int TH = tile_rows(SCAN);   // tile rows
   constexpr int NPX = kTile * TH;       // pool pixels
   __shared__ unsigned long long s_acc[NPX * 3];
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if (threadIdx.x == 0) s_pool_next = (SCAN == SCAN_BVHQ && !STATS) ? 0 : 256;   // (the ring claims its own)
+  if (threadIdx.x == 0) s_pool_next = kRing ? 0 : 256;   // (the ring claims its own)
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
   if constexpr (SRC == SRC_LDS) {
     if constexpr (is_bvh_scan(SCAN)) {
@@ -328,8 +345,11 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // image has no room for it: C4 keeps 5 workgroups per CU)
   // (the ring below takes the pixel arithmetic out of the loop altogether:
   // only the statistics build of this traversal keeps the table)
-  constexpr bool kRing = SCAN == SCAN_BVHQ && !STATS;
+#ifdef RTCLJ_AB_NO_RING
+  constexpr bool kPixelTable = false;
+#else
   constexpr bool kPixelTable = SCAN == SCAN_BVHQ && !kRing;
+#endif
   __shared__ float4 s_px[kPixelTable ? NPX : 1];
   if constexpr (kPixelTable) {
     const int t = static_cast<int>(threadIdx.x);
