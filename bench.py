@@ -480,7 +480,7 @@ def main():
             "dispatch_order": {"kernel_ms": mine["first_launch_ms"],
                                "note": "the same frame with tiles in plain dispatch order (rt_set_schedule(1)), as a "
                                        "launch of a new shape runs (no tile costs yet); the timed steps dispatch "
-                                       "longest first by the previous launch's per-tile durations"},
+                                       "longest first by the previous launches' per-tile durations (each added to half the record before it)"},
             "per_rank": {"kernel_ms_avg": kms, "rows": [r["rows"] for r in per_rank],
                          "imbalance": max(kms) / (sum(kms) / len(kms)),
                          "elapsed_ms": [r["elapsed_s"] * 1e3 for r in per_rank],

@@ -248,9 +248,9 @@ int rt_resolve_variant(const rt_dscene* ds);
 int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int* out4);
 
 /* Tile dispatch order of rt_launch.  0 (default) = adaptive: every launch
- * records how long each 8 x 8 pixel tile's waves ran, and a one-block sort
- * enqueued after it (same stream, no host sync) turns that into a
- * longest-first order; the next launch on the same scene and stream with the
+ * adds how long each 8 x 8 pixel tile's waves ran to half the tile's earlier
+ * record, and a one-block sort enqueued after it (same stream, no host sync)
+ * turns that into a longest-first order; the next launch on the same scene and stream with the
  * same launch shape (width, row selection; camera, spp, seed, flags and the
  * kernel variant may differ) dispatches its tiles in that order, so the slow
  * tiles do not trail the kernel's end.  A launch of another shape runs in

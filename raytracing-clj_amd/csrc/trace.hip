@@ -79,7 +79,7 @@ struct alignas(16) KArgs {
   int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: tile order (longest first) -> tile
-  unsigned* tile_cost;     // nullable: per tile, its workgroups' durations summed (s_memrealtime ticks)
+  unsigned* tile_cost;     // nullable: per tile, its workgroups' durations added (s_memrealtime ticks) to half the history
   // Work units: the first n_whole tiles of the order are one
   // workgroup each, every later tile is `split` workgroups, one contiguous
   // sample range each, whose integer pixel sums go to part[split index]
@@ -1258,13 +1258,16 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
 // The adaptive schedule's sort: tile indices by descending cost (a counting
 // sort over 256 log-scale buckets: the top 5 bits are the cost's bit length,
 // the low 3 the bits below its leading one).  One block; the order within a
-// bucket is arbitrary (any order renders the same bits).
+// bucket is arbitrary (any order renders the same bits).  Each cost is then
+// halved, so the next launch sorts by its own durations plus half of this
+// history (a decayed mean: a tile's cost depends on what shared its CU;
+// profiles/r02/shard_cost_decay.txt).
 __device__ __forceinline__ int cost_bucket(unsigned c) {
   if (c < 8) return static_cast<int>(c);
   const int e = 31 - __clz(c);                                  // 3..31
   return ((e - 2) << 3) | static_cast<int>((c >> (e - 3)) & 7u); // monotone, < 256
 }
-__global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict__ cost, int* __restrict__ order,
+__global__ __launch_bounds__(1024) void order_kernel(unsigned* __restrict__ cost, int* __restrict__ order,
                                                      int n) {
   __shared__ int hist[256];
   __shared__ int cursor[256];
@@ -1280,7 +1283,11 @@ __global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict_
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += 1024) order[atomicAdd(&cursor[cost_bucket(cost[i])], 1)] = i;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const unsigned c = cost[i];
+    order[atomicAdd(&cursor[cost_bucket(c)], 1)] = i;
+    cost[i] = c >> 1;   // the next launch adds its durations to half of these
+  }
 }
 
 // The split tiles' pixels (order positions [n_whole, n_tiles)): the sum of
@@ -1862,7 +1869,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     a.part = sch->part;
   }
   // adaptive schedule: dispatch tiles longest first, by the durations the
-  // previous launch of this launch shape on this scene and stream measured
+  // previous launches of this launch shape on this scene and stream measured
+  // (each launch's added to half the record before it)
   if (sch && g_schedule.load() == 0) {
     ScheduleKey key{};
     key.width = a.width;
@@ -1891,7 +1899,9 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     }
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
-    HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
+    // the costs decay (order_kernel halves them after sorting): zeroed only
+    // when this launch shape starts a new history
+    if (!sch->ready) HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
   }
   void* args[] = {&a};
   HIP_TRY(hipLaunchKernel(v.fn, dim3(n_units), block, args, lds, stream));
@@ -1906,7 +1916,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   if (a.tile_cost) {
     // the next launch's order, stream-ordered after this kernel (no host sync)
-    const unsigned* cost = sch->cost;
+    unsigned* cost = sch->cost;
     int* order = sch->order;
     int n = n_tiles;
     void* sargs[] = {&cost, &order, &n};

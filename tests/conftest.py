@@ -16,6 +16,12 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def gpu_lib():
     """The product library with at least one visible GPU (fails loudly otherwise)."""
+    # torch's wheel bundles its own HIP runtime under the same soname
+    # (libamdhip64.so.7) as /opt/rocm's, which librtclj.so links: whichever
+    # loads first serves the process, and torch fails to initialise on the
+    # /opt/rocm one ("No HIP GPUs are available"). Tests that use torch
+    # buffers therefore load torch first, as bench.py does.
+    import torch  # noqa: F401
     import rtclj
 
     n = rtclj.lib.rt_device_count()
