@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--variant", type=int, default=16, help="16: the default traversal (timeline only); 17: with counters (~16x slower)")
     ap.add_argument("--bins", type=int, default=20)
+    ap.add_argument("--warm", type=int, default=1, help="untimed launches before the recorded one (the adaptive order's history)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
@@ -64,7 +65,8 @@ def main():
     def launch():
         check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), C.c_void_p(cnt.data_ptr()), sh))
 
-    launch()   # warm-up: the adaptive order for the next launch
+    for _ in range(a.warm):   # warm-up: the adaptive order's record for the next launch
+        launch()
     torch.cuda.synchronize()
     st = (C.c_uint64 * 32)()
     check(lib.rt_debug_stats(st))
@@ -95,7 +97,7 @@ def main():
         ov = np.clip(np.minimum(end, hi) - np.maximum(start, lo), 0, None)
         busy.append(float(ov.sum() / (hi - lo)))
     res = {
-        "workload": a.workload, "world": a.world, "rank": a.rank, "variant": a.variant,
+        "workload": a.workload, "world": a.world, "rank": a.rank, "variant": a.variant, "warm": a.warm,
         "kernel_ms_event": ms, "span_us": float(span), "waves": int(len(w)),
         "occupancy_api": list(occ),
         "wave_us": {"mean": float(dur.mean()), "p50": float(np.median(dur)), "p95": float(np.percentile(dur, 95)),
