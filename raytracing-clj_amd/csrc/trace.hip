@@ -216,6 +216,8 @@ struct alignas(16) Pair {
   f2 x, y, z, w;   // centres and -r^2 of bodies 2p and 2p+1
 };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc_lo(f2 v) { return __builtin_shufflevector(v, v, 0, 0); }
+__device__ __forceinline__ f2 bc_hi(f2 v) { return __builtin_shufflevector(v, v, 1, 1); }
 
 // BVH node as the kernel reads it (= rtclj::BvhNode, bvh.h): per axis the
 // (child0, child1) pairs (min, max, min); a ray's (near, far) planes are the
@@ -234,32 +236,22 @@ constexpr int kTile = 8;
 constexpr int kPoolPx = kTile * kTile;
 constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : kTile; }
 
-// A/B builds only ("six waves per SIMD"): -DRTCLJ_AB_WAVES6
-// caps the registers at 80 (6 waves per SIMD, with spills); -DRTCLJ_AB_NO_RING
-// makes camera samples in the loop without the pixel table, so that the
-// default traversal's LDS image fits 6 workgroups per CU
 template <int SRC, int SCAN, bool STATS = false>
-#ifdef RTCLJ_AB_WAVES6
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void trace_kernel(const KArgs a) {
-#else
 __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
-#endif
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
   // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample
   // j / npx: the lanes ending paths together add into different pixels'
-  // sums).  Camera samples come from per-wave rings in LDS (default
-  // traversal) or, in the other traversals, a lane whose path ends takes the
-  // next index from an LDS counter (one ds_add per wave event, then an mbcnt
-  // prefix).  The colour sums are u64 per pixel and channel in LDS, added
-  // with ds_add_u64: order-free.
+  // sums).  A lane whose path ends takes the next index from an LDS counter
+  // (one ds_add per wave event, then an mbcnt prefix).  The colour sums are
+  // u64 per pixel and channel in LDS, added with ds_add_u64: order-free.
   __shared__ int s_pool_next;
-  // camera samples from per-wave rings in LDS (below), for the default
-  // traversal; the other traversals and the statistics build make them in
-  // the loop
-#ifdef RTCLJ_AB_NO_RING
-  constexpr bool kRing = false;
-#else
+  // A/B build only (-DRTCLJ_AB_RING): camera samples made in
+  // per-wave batches into LDS rings.  Worth 2.6 % at 5 workgroups per CU,
+  // but its 5 KB of LDS keep the default traversal from the sixth (§8)
+#ifdef RTCLJ_AB_RING
   constexpr bool kRing = SCAN == SCAN_BVHQ && !STATS;
+#else
+  constexpr bool kRing = false;
 #endif
   constexpr int TH = tile_rows(SCAN);   // tile rows
   constexpr int NPX = kTile * TH;       // pool pixels
@@ -339,28 +331,6 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
-  // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
-  // key and coordinates, so a camera sample costs one LDS read instead of
-  // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
-  // image has no room for it: C4 keeps 5 workgroups per CU)
-  // (the ring below takes the pixel arithmetic out of the loop altogether:
-  // only the statistics build of this traversal keeps the table)
-#ifdef RTCLJ_AB_NO_RING
-  constexpr bool kPixelTable = false;
-#else
-  constexpr bool kPixelTable = SCAN == SCAN_BVHQ && !kRing;
-#endif
-  __shared__ float4 s_px[kPixelTable ? NPX : 1];
-  if constexpr (kPixelTable) {
-    const int t = static_cast<int>(threadIdx.x);
-    if (t < npx) {
-      const int qy = vw == 1 ? t : static_cast<int>(__umulhi(static_cast<uint32_t>(t), mag_vw));
-      const int px = qx0 + (t - qy * vw);
-      const int gy = image_row(qy0 + qy);
-      s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
-    }
-    __syncthreads();
-  }
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
   bool active = kRing ? true : j < pool;
 
@@ -515,25 +485,15 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           st_fresh_lanes += __popcll(ex);
         }
       }
-      // pool index -> (pixel, sample), sample-major as the ring's batches:
-      // the lanes ending paths together add into different pixels' sums
+      // pool index -> (pixel, sample), sample-major: the lanes ending paths
+      // together add into different pixels' sums
       k = div_magic(j, npx_magic);
       q = j - k * npx;
-      uint32_t pk;
-      float fpx, fgy;
-      if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
-        const float4 pt = s_px[q];
-        pk = __float_as_uint(pt.x);
-        fpx = pt.y;
-        fgy = pt.z;
-      } else {
-        const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
-        const int px = qx0 + (q - qy * vw);
-        const int gy = image_row(qy0 + qy);
-        pk = pixel_key(px, gy);
-        fpx = static_cast<float>(px);
-        fgy = static_cast<float>(gy);
-      }
+      const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
+      const int px = qx0 + (q - qy * vw);
+      const int gy = image_row(qy0 + qy);
+      const uint32_t pk = pixel_key(px, gy);
+      const float fpx = static_cast<float>(px), fgy = static_cast<float>(gy);
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
       st = mix32(pk + static_cast<uint32_t>(a.sample_begin + k0 + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
@@ -677,19 +637,20 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const float rux = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(ux), -1e24f, 1e24f);
       const float ruy = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(uy), -1e24f, 1e24f);
       const float ruz = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(uz), -1e24f, 1e24f);
-      const f2 ix2 = {rux, rux}, iy2 = {ruy, ruy}, iz2 = {ruz, ruz};
+      // broadcast operands as halves of packed pairs (bc_lo / bc_hi: one
+      // register read through op_sel for both halves, not a duplicated pair)
+      f2 r_xy = {rux, ruy}, r_z = {ruz, ruz};
       // the min plane's bound b*(1/u) - (o' + P)/u, the max plane's
       // b*(1/u) - (o' - P)/u; by the sign of 1/u one is the near plane
       const float nlx = -(ecx + P) * rux, nly = -(ecy + P) * ruy, nlz = -(ecz + P) * ruz;
       const float nhx = -(ecx - P) * rux, nhy = -(ecy - P) * ruy, nhz = -(ecz - P) * ruz;
       const bool sx = rux < 0.0f, sy = ruy < 0.0f, sz = ruz < 0.0f;
-      const f2 nearx = {sx ? nhx : nlx, sx ? nhx : nlx}, farx = {sx ? nlx : nhx, sx ? nlx : nhx};
-      const f2 neary = {sy ? nhy : nly, sy ? nhy : nly}, fary = {sy ? nly : nhy, sy ? nly : nhy};
-      const f2 nearz = {sz ? nhz : nlz, sz ? nhz : nlz}, farz = {sz ? nlz : nhz, sz ? nlz : nhz};
+      f2 nf_x = {sx ? nhx : nlx, sx ? nlx : nhx};   // (near, far) plane offsets
+      f2 nf_y = {sy ? nhy : nly, sy ? nly : nhy};
+      f2 nf_z = {sz ? nhz : nlz, sz ? nlz : nhz};
       // byte offsets of the (near, far) pairs of each axis inside a node
       const int offx = sx ? 8 : 0, offy = 24 + (sy ? 8 : 0), offz = 48 + (sz ? 8 : 0);
-      const f2 ox2 = {ox, ox}, oy2 = {oy, oy}, oz2 = {oz, oz};
-      const f2 ux2 = {ux, ux}, uy2 = {uy, uy}, uz2 = {uz, uz};
+      f2 o_xy = {ox, oy}, o_zux = {oz, ux}, u_yz = {uy, uz};
       // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
       // size 4), tested packed; the acceptance is order-independent
       auto leaf = [&](int p) {
@@ -717,8 +678,9 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
           if constexpr (STATS) st_fl += 32;   // 2 bodies x (oc 3, h 5, c 6, disc 2)
           const Pair g = lp[hb + q];
           const PidxT id = li[hb + q];
-          const f2 ocx = g.x - ox2, ocy = g.y - oy2, ocz = g.z - oz2;
-          const f2 h = fma2(uz2, ocz, fma2(uy2, ocy, ux2 * ocx));
+          asm volatile("" : "+v"(o_xy), "+v"(o_zux), "+v"(u_yz));
+          const f2 ocx = g.x - bc_lo(o_xy), ocy = g.y - bc_hi(o_xy), ocz = g.z - bc_lo(o_zux);
+          const f2 h = fma2(bc_hi(u_yz), ocz, fma2(bc_lo(u_yz), ocy, bc_hi(o_zux) * ocx));
           const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
           const f2 disc = fma2(h, h, -c);
           hh[2 * q] = h.x;
@@ -789,9 +751,10 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
         const f2* ay = reinterpret_cast<const f2*>(nb + offy);
         const f2* az = reinterpret_cast<const f2*>(nb + offz);
         const int2 ch = *reinterpret_cast<const int2*>(nb + 72);
-        const f2 tnx = fma2(ax[0], ix2, nearx), tfx = fma2(ax[1], ix2, farx);
-        const f2 tny = fma2(ay[0], iy2, neary), tfy = fma2(ay[1], iy2, fary);
-        const f2 tnz = fma2(az[0], iz2, nearz), tfz = fma2(az[1], iz2, farz);
+        asm volatile("" : "+v"(r_xy), "+v"(r_z), "+v"(nf_x), "+v"(nf_y), "+v"(nf_z));
+        const f2 tnx = fma2(ax[0], bc_lo(r_xy), bc_lo(nf_x)), tfx = fma2(ax[1], bc_lo(r_xy), bc_hi(nf_x));
+        const f2 tny = fma2(ay[0], bc_hi(r_xy), bc_lo(nf_y)), tfy = fma2(ay[1], bc_hi(r_xy), bc_hi(nf_y));
+        const f2 tnz = fma2(az[0], bc_lo(r_z), bc_lo(nf_z)), tfz = fma2(az[1], bc_lo(r_z), bc_hi(nf_z));
         tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
         const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
@@ -1636,16 +1599,16 @@ static size_t stack_of(const DTree& t, int tree) {
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
-// kernel's static LDS (pool counter, the 64 pixels' colour sums and the four
-// waves' camera-sample rings)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 4 * 5 * 64 * 4 + 12;   // (the 8-body traversal's 8x4 tile, no ring: 5.9 KB less)
+// kernel's static LDS (pool counter, the 64 pixels' colour sums).  (Its
+// registers allow 6; C1's 25.0 KB image fits 6 as well.)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;   // (the 8-body traversal's 8x4 tile: 0.8 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
 static int resolve_variant(const rt_dscene& ds, int vsel) {
   // default: 4-body leaves, unless that tree's LDS image limits a CU below
-  // the 5 workgroups the registers allow (160 KB / 5) and the 8-body-leaf
-  // tree's is smaller (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
+  // 5 workgroups (160 KB / 5) and the 8-body-leaf tree's is smaller
+  // (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
   if (vsel == 0)
     vsel = (lds_of(ds.tree[1], 1) > kLds5 && ds.tree[2].n_nodes <= 256 &&
             lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
