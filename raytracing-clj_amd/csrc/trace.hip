@@ -76,7 +76,7 @@ struct alignas(16) KArgs {
   int bvh_off_pidx;
   int big_pair0;         // the big bodies' leaves (bvh.cpp): pairs [big_pair0, + n_big_leaves x leaf pairs)
   int n_big_leaves;
-  int bvh_stack;         // stack entries per lane (tree depth + 2, <= kBvhStack)
+  int bvh_stack;         // stack entries per lane (stack_entries: tree depth, or + 2 for tree 0)
   float bvh_c[3], bvh_r; // bounding sphere of the tree's bodies
   const int* tile_order;   // nullable: tile order (longest first) -> tile
   unsigned* tile_cost;     // nullable: per tile, its workgroups' durations added (s_memrealtime ticks) to half the history
@@ -331,6 +331,22 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
+  // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
+  // key and coordinates, so a camera sample costs one LDS read instead of
+  // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
+  // image has no room for it: C4 keeps 5 workgroups per CU)
+  constexpr bool kPixelTable = SCAN == SCAN_BVHQ && !kRing;
+  __shared__ float4 s_px[kPixelTable ? NPX : 1];
+  if constexpr (kPixelTable) {
+    const int t = static_cast<int>(threadIdx.x);
+    if (t < npx) {
+      const int qy = vw == 1 ? t : static_cast<int>(__umulhi(static_cast<uint32_t>(t), mag_vw));
+      const int px = qx0 + (t - qy * vw);
+      const int gy = image_row(qy0 + qy);
+      s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
+    }
+    __syncthreads();
+  }
   int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
   bool active = kRing ? true : j < pool;
 
@@ -489,11 +505,21 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       // together add into different pixels' sums
       k = div_magic(j, npx_magic);
       q = j - k * npx;
-      const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
-      const int px = qx0 + (q - qy * vw);
-      const int gy = image_row(qy0 + qy);
-      const uint32_t pk = pixel_key(px, gy);
-      const float fpx = static_cast<float>(px), fgy = static_cast<float>(gy);
+      uint32_t pk;
+      float fpx, fgy;
+      if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
+        const float4 pt = s_px[q];
+        pk = __float_as_uint(pt.x);
+        fpx = pt.y;
+        fgy = pt.z;
+      } else {
+        const int qy = vw == 1 ? q : static_cast<int>(__umulhi(static_cast<uint32_t>(q), mag_vw));
+        const int px = qx0 + (q - qy * vw);
+        const int gy = image_row(qy0 + qy);
+        pk = pixel_key(px, gy);
+        fpx = static_cast<float>(px);
+        fgy = static_cast<float>(gy);
+      }
       // ---- compute-pixel, one sample (raytracing.clj:144-151) ----
       st = mix32(pk + static_cast<uint32_t>(a.sample_begin + k0 + k) * 0x9e3779b9u);
       if (st == 0) st = 0x6d2b79f5u;
@@ -1594,14 +1620,15 @@ extern "C" int rt_scene_free(rt_dscene* d) {
 
 // traversal stack bytes: u8 entries for the 8-body-leaf tree (tree[2], at
 // most 256 nodes when its variant runs), u16 otherwise
+static int stack_entries(const DTree& t, int tree) { return tree == 0 ? t.depth + 2 : std::max(t.depth, 1); }
 static size_t stack_of(const DTree& t, int tree) {
-  return static_cast<size_t>(t.depth + 2) * 256 * (tree == 2 ? 1 : 2);
+  return static_cast<size_t>(stack_entries(t, tree)) * 256 * (tree == 2 ? 1 : 2);
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
-// kernel's static LDS (pool counter, the 64 pixels' colour sums).  (Its
-// registers allow 6; C1's 25.0 KB image fits 6 as well.)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + 12;   // (the 8-body traversal's 8x4 tile: 0.8 KB less)
+// kernel's static LDS (pool counter, the 64 pixels' colour sums and pixel
+// table).  (Its registers allow 6; C1's 24.0 KB image fits 6 as well.)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal's 8x4 tile, no table: 1.8 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs
@@ -1755,7 +1782,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.bvh_off_pidx = tr.off_pidx;
   a.big_pair0 = tr.big_pair0;
   a.n_big_leaves = tr.n_big_leaves;
-  a.bvh_stack = tr.depth + 2;   // ordered traversal holds <= depth, while-while <= depth + 2
+  // entries per lane: the ordered traversal (trees 1, 2) holds at most depth
+  // (a node on level L has L - 1 ancestors; the dead far-child write goes one
+  // above them); tree 0 also serves the while-while variants (depth + 2)
+  a.bvh_stack = stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
