@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   int last = -1;   // body the current ray leaves (-1: camera ray)
   bool fresh = !kRing;
 
-  // ---- camera-sample ring (4-body-leaf traversal) ----
+  // ---- camera-sample ring (A/B build -DRTCLJ_AB_RING only) ----
   // Each wave keeps up to 64 camera samples ready in LDS ([field][slot]: RNG
   // state after the sample's draws, fx, fy, the disk draws' 24-bit integers
   // with the pool pixel in the top byte of the first).  A wave whose lanes
