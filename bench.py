@@ -302,6 +302,7 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=3):
             "upload_ms": best["upload_ms"], "gather_ms": best["gather_ms"], "scene_cached": best["scene_cached"],
             "value": W * H * spp / (best["total_ms"] * 1e-3) / 1e6, "unit": "Mray-samples/s",
             "first_call": {"total_ms": first["total_ms"], "upload_ms": first["upload_ms"],
+                           "kernel_ms_max": first["kernel_ms"], "gather_ms": first["gather_ms"],
                            "scene_cached": first["scene_cached"], "python_wall_ms": first_wall},
             "repeats": reps}, out
 
