@@ -69,8 +69,9 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed frames (default: 100 for c1, a ~0.6 s GPU region; 5 for the larger workloads)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed frames (default: 5 for c1, 1 otherwise)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
     ap.add_argument("--spp", type=int, default=None, help="override the workload's spp (not a bench line)")
@@ -83,7 +84,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--e2e", choices=["auto", "off"], default="auto", help="time rt_render end to end on rank 0")
     ap.add_argument("--stats", choices=["auto", "off"], default="auto", help="one untimed stats-build launch")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 100 if a.workload == "c1" else 5
+    if a.warmup is None:
+        a.warmup = 5 if a.workload == "c1" else 1
+    return a
 
 
 def host_cpus():

@@ -96,6 +96,11 @@ def test_bench_defaults_to_row_tile_strong_scaling(monkeypatch):
     bench = importlib.import_module("bench")
     a = bench.parse()
     assert a.scaling == "strong" and a.workload == "c1"
+    assert (a.steps, a.warmup) == (100, 5)   # c1: a ~0.6 s timed GPU region
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "c4"])
+    b = bench.parse()
+    assert (b.steps, b.warmup) == (5, 1)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
     from rtclj.shard import shard_params
     p0 = shard_params(2, 0, 1200, 675, 100, 50, scaling=a.scaling)
     p1 = shard_params(2, 1, 1200, 675, 100, 50, scaling=a.scaling)
