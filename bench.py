@@ -51,7 +51,14 @@ from rtclj import scenes  # noqa: E402
 from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0, check, diag_lib, lib, rt_params  # noqa: E402
 from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
+# BASELINE.json's metric is quoted on C1; the other workloads report the same
+# quantity at their own frame (metric_for)
 METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs peak"
+
+
+def metric_for(width, height, spp, depth):
+    return f"Mray-samples/sec at {width}×{height}×{spp}spp depth{depth}; achieved HBM GB/s vs peak"
+
 PMC_DIR = ROOT / "profiles" / "r02" / "pmc_c1"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
@@ -281,18 +288,25 @@ def occupancy(ds, p):
             "lds_bytes_per_wg": o[2], "variant": o[3], "hw_max_waves_per_simd": 8}
 
 
-def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=3):
+PARTS = ("upload_ms", "setup_ms", "enqueue_ms", "wait_ms", "scatter_ms", "other_ms")
+
+
+def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=5):
     """rt_render, the product entry point the JNI shim calls: the scene cache
     (the first call uploads and builds the BVHs), the N-device fan-out with
-    one host thread per device, D2H into pinned memory and the host gather
-    into one caller buffer.  Warm call first, then `reps` timed calls."""
+    one host thread per device, D2H and the host gather into one caller
+    buffer.  The first call of the process (rt_cache_clear() first, so it
+    pays the scene upload, the BVH builds and the device context set-up, as
+    the reference's one-frame `-main` does), then `reps` timed calls whose
+    median is the value (min and max beside it).  `parts` are rt_stats' host
+    clocks of the slowest device's share; they add up to total_ms."""
     import numpy as np
     visible = lib.rt_device_count()
     flags = RT_FLAG_SHARDS_ON_DEVICE0 if n_dev > visible else 0
-    out = np.empty((H, W, 3), np.float32)
+    lib.rt_cache_clear()
     first = {}
     t0 = time.perf_counter()
-    R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=first)
+    out = R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=first)
     first_wall = (time.perf_counter() - t0) * 1e3
     runs = []
     for _ in range(reps):
@@ -301,16 +315,53 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=3):
         out = R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=st)
         st["wall_ms"] = (time.perf_counter() - t0) * 1e3
         runs.append(st)
-    best = min(runs, key=lambda r: r["total_ms"])
-    return {"entry": "rt_render (include/rt.h)", "n_devices": best["n_devices"],
-            "shards_on_device0": bool(flags), "total_ms": best["total_ms"], "kernel_ms_max": best["kernel_ms"],
-            "kernel_ms_mean": best["kernel_ms_mean"], "imbalance": best["kernel_ms"] / best["kernel_ms_mean"],
-            "upload_ms": best["upload_ms"], "gather_ms": best["gather_ms"], "scene_cached": best["scene_cached"],
-            "value": W * H * spp / (best["total_ms"] * 1e-3) / 1e6, "unit": "Mray-samples/s",
-            "first_call": {"total_ms": first["total_ms"], "upload_ms": first["upload_ms"],
-                           "kernel_ms_max": first["kernel_ms"], "gather_ms": first["gather_ms"],
-                           "scene_cached": first["scene_cached"], "python_wall_ms": first_wall},
+    runs.sort(key=lambda r: r["total_ms"])
+    med = runs[len(runs) // 2]
+
+    def parts(r):
+        return {k: r[k] for k in PARTS}
+
+    return {"entry": "rt_render (include/rt.h)", "n_devices": med["n_devices"],
+            "shards_on_device0": bool(flags), "statistic": f"median of {reps} calls",
+            "total_ms": med["total_ms"], "total_ms_min": runs[0]["total_ms"], "total_ms_max": runs[-1]["total_ms"],
+            "kernel_ms_max": med["kernel_ms"], "kernel_ms_mean": med["kernel_ms_mean"],
+            "imbalance": med["kernel_ms"] / med["kernel_ms_mean"], "d2h_ms": med["d2h_ms"],
+            "gather_ms": med["gather_ms"], "scene_cached": med["scene_cached"], "parts": parts(med),
+            "value": W * H * spp / (med["total_ms"] * 1e-3) / 1e6, "unit": "Mray-samples/s",
+            "first_call": {"total_ms": first["total_ms"], "parts": parts(first), "kernel_ms_max": first["kernel_ms"],
+                           "d2h_ms": first["d2h_ms"], "scene_cached": first["scene_cached"],
+                           "python_wall_ms": first_wall,
+                           "note": "the process's first rt_render after rt_cache_clear(): scene upload + BVH builds "
+                                   "(upload_ms), the device context (setup_ms: stream, events, framebuffer, pinned "
+                                   "counters), the launch enqueue (enqueue_ms; the first launch of a kernel loads "
+                                   "its code object), the device work (wait_ms: kernel in plain tile order + D2H)"},
             "repeats": reps}, out
+
+
+def first_process(wl, spp, depth, seed, n_dev):
+    """The reference's own usage, one frame per process (`clojure -M:main`,
+    raytracing.clj:95-177): lib/rt_main, the C++ host of the C ABI, run as a
+    fresh child process on this workload (the cover scene), --json: the HIP
+    runtime's start-up (first rt_device_count), rt_render's parts on a cold
+    library (scene upload + BVHs, device context, first launch = code-object
+    load, kernel in plain tile order + D2H), quantise and the PPM write."""
+    import subprocess
+    import tempfile
+    exe = ROOT / "raytracing-clj_amd" / "lib" / "rt_main"
+    if wl["scene"] != "cover11" or not exe.exists():
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        t0 = time.perf_counter()
+        r = subprocess.run([str(exe), str(spp), str(depth), "--scene", "cover", "--width", str(wl["width"]),
+                            "--seed", str(seed), "--gpus", str(n_dev), "--out", str(Path(td) / "scene.ppm"), "--json"],
+                           capture_output=True, text=True, timeout=300)
+        wall = (time.perf_counter() - t0) * 1e3
+    if r.returncode != 0:
+        return {"error": (r.stdout + r.stderr)[-400:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    d["child_wall_ms"] = wall
+    d["command"] = f"rt_main {spp} {depth} --scene cover --width {wl['width']} --seed {seed} --gpus {n_dev} --json"
+    return d
 
 
 def main():
@@ -467,7 +518,7 @@ def main():
         hbm_bytes = rows * W * 12 + len(scene) * 32
         gbs = hbm_bytes / (kern_avg_ms * 1e-3) / 1e9
         res = {
-            "metric": METRIC, "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC if (a.workload == "c1" and not a.spp) else metric_for(W, H, spp, depth), "value": value, "unit": "Mray-samples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": a.scaling, "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic: RTIOW cover scene ({len(scene)} bodies, generator seed 42), render seed {a.seed}",
@@ -503,6 +554,8 @@ def main():
         barrier()
         if rank == 0:
             res["end_to_end"], frame = end_to_end(scene, cam, W, H, spp, depth, a.seed, world)
+            if world == 1:
+                res["end_to_end"]["first_process"] = first_process(wl, spp, depth, a.seed, world)
         barrier()
     if rank == 0:
         if a.cpu_baseline == "auto" and world == 1:

@@ -37,6 +37,11 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
+/* ABI revision of this header (rt_abi_version() of the loaded library must
+ * equal it; INTEGRATION.md lists the breaks).  3: rt_stats grew to 112 bytes
+ * (set-up/enqueue/wait/scatter/other/D2H timers). */
+#define RT_ABI_VERSION 3
+
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
   RT_OK = 0,
@@ -135,6 +140,18 @@ typedef struct rt_stats {
                              scatter of the device's row tiles into out_rgb    */
   double kernel_ms_mean;  /* mean over devices of the trace-kernel time
                              (load imbalance = kernel_ms / kernel_ms_mean)     */
+  /* Where the wall time of the slowest device's share went (host clocks, in
+   * order): upload_ms above, then these; the rest of total_ms (argument
+   * checks, thread fan-out and join) is other_ms.  A first call shows its
+   * one-time costs here: setup_ms (the device's stream, events, device
+   * framebuffer, pinned buffers) and enqueue_ms (the first launch loads the
+   * kernels' code object).                                                   */
+  double setup_ms;        /* render context set-up                             */
+  double enqueue_ms;      /* rt_launch + D2H enqueue                           */
+  double wait_ms;         /* host wait for the device: kernel + D2H            */
+  double scatter_ms;      /* host scatter of row tiles (several devices)       */
+  double other_ms;        /* total_ms - upload - setup - enqueue - wait - scatter */
+  double d2h_ms;          /* max over devices: event-timed D2H of the frame    */
 } rt_stats;
 
 /* ========================= host-side helpers =========================== */
@@ -287,6 +304,7 @@ int rt_debug_waves(int device, uint64_t* out, size_t n_waves);
 int rt_device_count(void);
 const char* rt_last_error(void);
 const char* rt_version(void);
+int rt_abi_version(void);   /* RT_ABI_VERSION the library was built with */
 
 #if defined(__GNUC__)
 #pragma GCC visibility pop

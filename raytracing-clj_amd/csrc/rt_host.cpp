@@ -158,7 +158,9 @@ extern "C" int rt_device_count(void) {
 
 extern "C" const char* rt_last_error(void) { return t_err.c_str(); }
 
-extern "C" const char* rt_version(void) { return "rtclj-mi355x 0.1 (gfx950)"; }
+extern "C" const char* rt_version(void) { return "rtclj-mi355x 0.3 (gfx950, abi 3)"; }
+
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 namespace {
 
@@ -210,7 +212,10 @@ struct Ctx {
   uint64_t* h_cnt = nullptr;  // pinned
   ~Ctx() {
     (void)hipSetDevice(device);
-    if (stream) (void)hipStreamSynchronize(stream);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      release_stream_schedules(device, stream);   // the scenes' per-stream slots
+    }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (e2) (void)hipEventDestroy(e2);
@@ -223,10 +228,14 @@ struct Ctx {
 };
 
 constexpr int kSceneCache = 4;   // scenes kept per device (least recently used out)
-constexpr int kFreeCtx = 4;      // idle contexts kept per device
+// idle contexts kept per device: as many as a scene has per-stream schedule
+// slots (trace.hip kSchedStreams), so RT_FLAG_SHARDS_ON_DEVICE0 with 8 shards
+// keeps its 8 streams and their tile orders from call to call
+constexpr int kFreeCtx = 8;
 
 struct DeviceCache {
   std::mutex mu;
+  std::mutex upload_mu;   // one upload at a time: concurrent misses of one scene build it once
   std::vector<CachedScene> scenes;
   std::vector<std::unique_ptr<Ctx>> free_ctx;
   uint64_t tick = 0;
@@ -235,20 +244,27 @@ struct DeviceCache {
 std::vector<DeviceCache>* g_cache = new std::vector<DeviceCache>(64);
 std::mutex g_cache_mu;
 
-// the cached device scene of s on `device`, uploading it on a miss
+// the cached device scene of s on `device`, uploading it on a miss.  Shards
+// of one call that share a device (RT_FLAG_SHARDS_ON_DEVICE0) and concurrent
+// calls miss together: the first uploads under upload_mu, the others wait for
+// it and then find its entry.
 int get_scene(int device, const rt_scene* s, std::shared_ptr<rt_dscene>* out, bool* hit) {
   DeviceCache& dc = (*g_cache)[device];
   const uint64_t h = scene_hash(*s);
-  {
+  auto lookup = [&]() {
     std::lock_guard<std::mutex> lk(dc.mu);
     for (CachedScene& c : dc.scenes)
       if (c.hash == h && same_scene(c, *s)) {
         c.last_use = ++dc.tick;
         *out = c.ds;
         *hit = true;
-        return RT_OK;
+        return true;
       }
-  }
+    return false;
+  };
+  if (lookup()) return RT_OK;
+  std::lock_guard<std::mutex> up(dc.upload_mu);
+  if (lookup()) return RT_OK;
   rt_dscene* raw = nullptr;
   const int rc = rt_scene_upload(device, s, &raw);
   if (rc != RT_OK) return rc;
@@ -301,8 +317,10 @@ struct Shard {
   int status = RT_OK;
   std::string err;
   uint64_t counters[2] = {0, 0};
-  float ms = 0.0f;
-  double upload_ms = 0.0, gather_ms = 0.0;
+  float ms = 0.0f, d2h_ms = 0.0f;
+  // host clocks of the share, in order (rt_stats)
+  double upload_ms = 0.0, setup_ms = 0.0, enqueue_ms = 0.0, wait_ms = 0.0, scatter_ms = 0.0, wall_ms = 0.0;
+  double gather_ms = 0.0;   // d2h_ms + scatter_ms
   bool cached = false;
 };
 
@@ -324,6 +342,7 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
   int rc = get_scene(sh->device, s, &ds, &sh->cached);
   if (rc != RT_OK) return fail(rc);
   sh->upload_ms = ms_since(t0);
+  const auto t_setup = Clock::now();
   std::unique_ptr<Ctx> cx = take_ctx(sh->device);
   const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
   hipError_t e = hipSetDevice(sh->device);
@@ -347,6 +366,8 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
     e = hipHostMalloc(&cx->h_pin, std::max<size_t>(nfl, 1) * sizeof(float), hipHostMallocDefault);
     if (e == hipSuccess) cx->h_cap = nfl;
   }
+  sh->setup_ms = ms_since(t_setup);
+  const auto t_enq = Clock::now();
   if (e == hipSuccess) e = hipMemsetAsync(cx->d_cnt, 0, 2 * sizeof(uint64_t), cx->stream);
   if (e == hipSuccess) e = hipEventRecord(cx->e0, cx->stream);
   if (e != hipSuccess) {
@@ -367,10 +388,14 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
       if (e == hipSuccess)
         e = hipMemcpyAsync(cx->h_cnt, cx->d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, cx->stream);
       if (e == hipSuccess) e = hipEventRecord(cx->e2, cx->stream);
+      sh->enqueue_ms = ms_since(t_enq);
+      const auto t_wait = Clock::now();
       if (e == hipSuccess) e = hipStreamSynchronize(cx->stream);
+      sh->wait_ms = ms_since(t_wait);
       float d2h = 0.0f;
       if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, cx->e0, cx->e1);
       if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->e1, cx->e2);
+      sh->d2h_ms = d2h;
       if (e != hipSuccess) {
         hip_fail(e, "rt_render trace/gather");
       } else {
@@ -389,10 +414,12 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
             ro += nr;
           }
         }
-        sh->gather_ms = d2h + ms_since(ts);
+        sh->scatter_ms = ms_since(ts);
+        sh->gather_ms = d2h + sh->scatter_ms;
       }
     }
   }
+  sh->wall_ms = ms_since(t0);
   if (sh->status == RT_OK) give_ctx(std::move(cx));
 }
 
@@ -464,12 +491,14 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     for (int d = 0; d < ndev; ++d) th.emplace_back(run_shard, s, c, &shards[d], out_rgb, rows, ntiles, ndev, d);
     for (auto& t : th) t.join();
   }
-  double kms = 0, ksum = 0, ums = 0, gms = 0;
+  double kms = 0, ksum = 0, ums = 0, gms = 0, d2h = 0;
   uint64_t segs = 0, smp = 0;
-  int cached = 0;
+  int cached = 0, slowest = 0;
   for (int d = 0; d < ndev; ++d) {
     Shard& sh = shards[d];
     if (sh.status != RT_OK) return set_error(sh.status, "device " + std::to_string(d) + ": " + sh.err);
+    if (sh.wall_ms > shards[slowest].wall_ms) slowest = d;
+    d2h = std::max(d2h, static_cast<double>(sh.d2h_ms));
     kms = std::max(kms, static_cast<double>(sh.ms));
     ksum += sh.ms;
     ums = std::max(ums, sh.upload_ms);
@@ -487,7 +516,14 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     stats->gather_ms = gms;
     stats->scene_cached = cached;
     stats->n_devices = ndev;
+    const Shard& sl = shards[slowest];
+    stats->setup_ms = sl.setup_ms;
+    stats->enqueue_ms = sl.enqueue_ms;
+    stats->wait_ms = sl.wait_ms;
+    stats->scatter_ms = sl.scatter_ms;
+    stats->d2h_ms = d2h;
     stats->total_ms = ms_since(t0);
+    stats->other_ms = stats->total_ms - (sl.upload_ms + sl.setup_ms + sl.enqueue_ms + sl.wait_ms + sl.scatter_ms);
   }
   return RT_OK;
 }

@@ -34,4 +34,10 @@ inline uint32_t seed_key(uint64_t seed) {
 // Rows produced by a row selection (contiguous or interleaved tiles).
 int rows_out(const rt_params& p);
 
+// rt_render's contexts own their streams: before one destroys its stream
+// (already synchronised) it drops that stream's adaptive-schedule and
+// split-sum entries from every live device scene of `device` (trace.hip), so
+// the scenes' per-stream slots do not fill up with dead streams.
+void release_stream_schedules(int device, void* stream);
+
 }  // namespace rtclj

@@ -8,8 +8,11 @@
 // frame as a PNG (rt_write_png; what src/ppm2png.clj produces).
 //
 //   rt_main [spp] [depth] [--scene reference|cover] [--realm] [--width W]
-//           [--seed S] [--gpus N] [--out PATH] [--png PATH]
+//           [--seed S] [--gpus N] [--out PATH] [--png PATH] [--json]
 // Defaults follow the reference: spp 100, depth 50, width 400, 16:9.
+// --json: one more line, a JSON object of where this one-frame process's time
+// went (the first rt_device_count starts the HIP runtime; rt_render's
+// rt_stats parts; quantise and file writes) -- bench.py's first_call.
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -25,8 +28,12 @@ int main(int argc, char** argv) {
   int spp = 100, depth = 50, width = 400, gpus = 0, grid = 11;
   unsigned long long seed = 1;
   std::string scene = "reference", out, png;
-  bool realm = false;
+  bool realm = false, json = false;
   int pos = 0;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto ms_since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto val = [&]() -> const char* {
@@ -44,6 +51,7 @@ int main(int argc, char** argv) {
     else if (a == "--out") out = val();
     else if (a == "--png") png = val();
     else if (a == "--realm") realm = true;
+    else if (a == "--json") json = true;
     else if (pos == 0) spp = std::atoi(argv[i]), ++pos;   // (:96)
     else if (pos == 1) depth = std::atoi(argv[i]), ++pos; // (:97)
   }
@@ -79,6 +87,10 @@ int main(int argc, char** argv) {
     }
   }
   rt_scene s{n, sph.data(), kind.data(), mat.data()};
+  const double scene_ms = ms_since(t_start);
+  const auto t_dev = std::chrono::steady_clock::now();
+  const int ndev = rt_device_count();   // the process's first HIP call: runtime start-up
+  const double device_count_ms = ms_since(t_dev);
   rt_params p{};
   p.width = width;
   p.height = height;
@@ -96,17 +108,32 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "rt_render failed: %s\n", rt_last_error());
     return 1;
   }
+  const double render_ms = ms_since(t0);
+  const auto t_q = std::chrono::steady_clock::now();
   std::vector<uint8_t> q(lin.size());
   rt_quantize(lin.data(), q.data(), q.size());
+  const double quantize_ms = ms_since(t_q);
+  const auto t_w = std::chrono::steady_clock::now();
   if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK ||
       (!png.empty() && rt_write_png(png.c_str(), q.data(), width, height) != RT_OK)) {
     std::fprintf(stderr, "%s\n", rt_last_error());
     return 1;
   }
+  const double write_ms = ms_since(t_w);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::printf("\"Elapsed time: %.3f msecs\"\n", ms);  // (time ...) (:99)
   std::printf("bodies %d, devices %d, kernel %.3f ms, %.1f Msamples/s, %.3f segments/sample\n", n,
               st.n_devices, st.kernel_ms, st.samples / (st.kernel_ms * 1e3),
               st.samples ? double(st.segments) / st.samples : 0.0);
+  if (json)
+    std::printf(
+        "{\"devices_visible\": %d, \"scene_ms\": %.3f, \"device_count_ms\": %.3f, \"render_ms\": %.3f, "
+        "\"quantize_ms\": %.3f, \"write_ms\": %.3f, \"process_ms\": %.3f, \"rt_stats\": {\"total_ms\": %.3f, "
+        "\"upload_ms\": %.3f, \"setup_ms\": %.3f, \"enqueue_ms\": %.3f, \"wait_ms\": %.3f, \"scatter_ms\": %.3f, "
+        "\"other_ms\": %.3f, \"kernel_ms\": %.3f, \"d2h_ms\": %.3f, \"segments\": %llu, \"samples\": %llu, "
+        "\"n_devices\": %d}}\n",
+        ndev, scene_ms, device_count_ms, render_ms, quantize_ms, write_ms, ms_since(t_start), st.total_ms,
+        st.upload_ms, st.setup_ms, st.enqueue_ms, st.wait_ms, st.scatter_ms, st.other_ms, st.kernel_ms, st.d2h_ms,
+        static_cast<unsigned long long>(st.segments), static_cast<unsigned long long>(st.samples), st.n_devices);
   return 0;
 }

@@ -1441,13 +1441,28 @@ struct ScheduleSet {
   std::mutex mu;
   int used = 0;
   Schedule s[kSchedStreams];
+  static void free_entry(Schedule& e) {
+    if (e.cost) (void)hipFree(e.cost);
+    if (e.order) (void)hipFree(e.order);
+    if (e.part) (void)hipFree(e.part);
+    e = Schedule{};
+  }
   void release() {
-    for (int k = 0; k < used; ++k) {
-      if (s[k].cost) (void)hipFree(s[k].cost);
-      if (s[k].order) (void)hipFree(s[k].order);
-      if (s[k].part) (void)hipFree(s[k].part);
-    }
+    for (int k = 0; k < used; ++k) free_entry(s[k]);
     used = 0;
+  }
+  // drop `stream`'s entry (its kernels have finished), keeping the others packed
+  void release_stream(hipStream_t stream) {
+    for (int k = 0; k < used; ++k)
+      if (s[k].stream == stream) {
+        free_entry(s[k]);
+        if (k != used - 1) {
+          s[k] = s[used - 1];
+          s[used - 1] = Schedule{};
+        }
+        --used;
+        return;
+      }
   }
 };
 
@@ -1464,6 +1479,19 @@ struct rt_dscene {
   int* kind;
   mutable ScheduleSet sched;   // rt_launch's adaptive tile order
 };
+
+// live device scenes, for release_stream_schedules (rt_host.cpp's contexts)
+static std::mutex g_scenes_mu;
+static std::vector<rt_dscene*> g_scenes;
+
+void rtclj::release_stream_schedules(int device, void* stream) {
+  std::lock_guard<std::mutex> lk(g_scenes_mu);
+  for (rt_dscene* d : g_scenes)
+    if (d->device == device) {
+      std::lock_guard<std::mutex> l2(d->sched.mu);
+      d->sched.release_stream(static_cast<hipStream_t>(stream));
+    }
+}
 
 static int hip_fail(hipError_t e, const char* what) {
   return set_error(RT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1598,12 +1626,20 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     rt_scene_free(d);
     return hip_fail(e, "rt_scene_upload");
   }
+  {
+    std::lock_guard<std::mutex> lk(g_scenes_mu);
+    g_scenes.push_back(d);
+  }
   *out = d;
   return RT_OK;
 }
 
 extern "C" int rt_scene_free(rt_dscene* d) {
   if (!d) return RT_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_scenes_mu);
+    g_scenes.erase(std::remove(g_scenes.begin(), g_scenes.end(), d), g_scenes.end());
+  }
   (void)hipSetDevice(d->device);
   if (d->geo) (void)hipFree(d->geo);
   if (d->geo2) (void)hipFree(d->geo2);

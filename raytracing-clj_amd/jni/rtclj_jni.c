@@ -42,28 +42,42 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_deviceCount(JNIEnv* env, jclass cls) {
 static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloatArray mats, jfloatArray camera,
                         jint defocus, jint width, jint height, jint spp, jint depth, jlong seed, jint n_gpus,
                         jint flags, jfloatArray out_rgb) {
+  if (!spheres || !kinds || !mats || !camera || !out_rgb) { /* Java nulls */
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
   const jsize n = (*env)->GetArrayLength(env, kinds);
-  if ((*env)->GetArrayLength(env, spheres) != 4 * n || (*env)->GetArrayLength(env, mats) != 4 * n ||
+  if ((*env)->GetArrayLength(env, spheres) / 4 != n || (*env)->GetArrayLength(env, spheres) % 4 != 0 ||
+      (*env)->GetArrayLength(env, mats) / 4 != n || (*env)->GetArrayLength(env, mats) % 4 != 0 ||
       (*env)->GetArrayLength(env, camera) != 18) {
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
   }
-  const jsize out_len = (*env)->GetArrayLength(env, out_rgb);
-  /* Copy every input; render into a malloc'd buffer and copy it back with
-   * SetFloatArrayRegion.  Nothing is pinned while rt_render runs (a full
-   * multi-GPU frame can take seconds: a critical section would block GC
-   * JVM-wide for that long). */
-  float* sph = (float*)(*env)->GetFloatArrayElements(env, spheres, NULL);
-  jint* knd = (*env)->GetIntArrayElements(env, kinds, NULL);
-  float* mat = (float*)(*env)->GetFloatArrayElements(env, mats, NULL);
-  float* out = (float*)malloc((size_t)out_len * sizeof(float) + 1);
-  float cam18[18];
-  (*env)->GetFloatArrayRegion(env, camera, 0, 18, cam18);
-  int rc = RT_E_ARG;
-  if (!sph || !knd || !mat || !out || (*env)->ExceptionCheck(env)) {
-    rc = RT_E_ARG; /* an OutOfMemoryError may already be pending */
-    goto done;
+  /* The frame is width x height x 3 floats; a longer Java array keeps its
+   * tail (only the frame is copied back), a shorter one is an argument error
+   * raised before anything is rendered. */
+  if (width <= 0 || height <= 0 || (*env)->GetArrayLength(env, out_rgb) / 3 / width < height) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
   }
+  const size_t frame = (size_t)width * (size_t)height * 3;
+  /* Copy every input; render into a malloc'd buffer and copy the frame back
+   * with SetFloatArrayRegion.  Nothing is pinned while rt_render runs (a full
+   * multi-GPU frame can take seconds: a critical section would block GC
+   * JVM-wide for that long).  A failed copy leaves an OutOfMemoryError
+   * pending: no further JNI call but the releases is made after it. */
+  float* sph = NULL;
+  jint* knd = NULL;
+  float* mat = NULL;
+  float* out = NULL;
+  float cam18[18];
+  int rc = RT_E_ARG;
+  if (!(sph = (float*)(*env)->GetFloatArrayElements(env, spheres, NULL))) goto done;
+  if (!(knd = (*env)->GetIntArrayElements(env, kinds, NULL))) goto done;
+  if (!(mat = (float*)(*env)->GetFloatArrayElements(env, mats, NULL))) goto done;
+  (*env)->GetFloatArrayRegion(env, camera, 0, 18, cam18);
+  if ((*env)->ExceptionCheck(env)) goto done;
+  if (!(out = (float*)malloc(frame * sizeof(float)))) goto done;
   rt_camera cam;
   memcpy(cam.center, cam18 + 0, 12);
   memcpy(cam.p00, cam18 + 3, 12);
@@ -84,8 +98,8 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   p.seed = (uint64_t)seed;
   p.n_devices = n_gpus;
   p.flags = flags;
-  rc = rt_render(&scene, &cam, &p, out, (size_t)out_len, NULL);
-  if (rc >= 0) (*env)->SetFloatArrayRegion(env, out_rgb, 0, out_len, out);
+  rc = rt_render(&scene, &cam, &p, out, frame, NULL);
+  if (rc >= 0) (*env)->SetFloatArrayRegion(env, out_rgb, 0, (jsize)frame, out);
 done:
   free(out);
   if (sph) (*env)->ReleaseFloatArrayElements(env, spheres, (jfloat*)sph, JNI_ABORT);
@@ -117,26 +131,34 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls
 JNIEXPORT jint JNICALL Java_rtclj_Native_writePng(JNIEnv* env, jclass cls, jstring path, jbyteArray rgb, jint width,
                                                   jint height) {
   (void)cls;
-  if ((jlong)(*env)->GetArrayLength(env, rgb) < (jlong)width * height * 3) {
+  if (!path || !rgb || width <= 0 || height <= 0 ||
+      (jlong)(*env)->GetArrayLength(env, rgb) < (jlong)width * height * 3) {
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
   }
+  int rc = RT_E_ARG;
+  jbyte* px = NULL;
   const char* p = (*env)->GetStringUTFChars(env, path, NULL);
-  jbyte* px = (*env)->GetByteArrayElements(env, rgb, NULL);
-  const int rc = (p && px) ? rt_write_png(p, (const uint8_t*)px, width, height) : RT_E_ARG;
+  if (p && (px = (*env)->GetByteArrayElements(env, rgb, NULL)) != NULL)
+    rc = rt_write_png(p, (const uint8_t*)px, width, height);
   if (px) (*env)->ReleaseByteArrayElements(env, rgb, px, JNI_ABORT);
   if (p) (*env)->ReleaseStringUTFChars(env, path, p);
-  if (rc < 0) throw_rt(env, rc);
+  if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_rt(env, rc);
   return rc;
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_ppmToPng(JNIEnv* env, jclass cls, jstring src, jstring dst) {
   (void)cls;
+  if (!src || !dst) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
+  int rc = RT_E_ARG;
+  const char* d = NULL;
   const char* s = (*env)->GetStringUTFChars(env, src, NULL);
-  const char* d = (*env)->GetStringUTFChars(env, dst, NULL);
-  const int rc = (s && d) ? rt_ppm_to_png(s, d) : RT_E_ARG;
+  if (s && (d = (*env)->GetStringUTFChars(env, dst, NULL)) != NULL) rc = rt_ppm_to_png(s, d);
   if (d) (*env)->ReleaseStringUTFChars(env, dst, d);
   if (s) (*env)->ReleaseStringUTFChars(env, src, s);
-  if (rc < 0) throw_rt(env, rc);
+  if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_rt(env, rc);
   return rc;
 }

@@ -60,7 +60,9 @@ class rt_params(C.Structure):
 class rt_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("kernel_ms", C.c_double),
                 ("total_ms", C.c_double), ("n_devices", C.c_int), ("scene_cached", C.c_int),
-                ("upload_ms", C.c_double), ("gather_ms", C.c_double), ("kernel_ms_mean", C.c_double)]
+                ("upload_ms", C.c_double), ("gather_ms", C.c_double), ("kernel_ms_mean", C.c_double),
+                ("setup_ms", C.c_double), ("enqueue_ms", C.c_double), ("wait_ms", C.c_double),
+                ("scatter_ms", C.c_double), ("other_ms", C.c_double), ("d2h_ms", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -94,7 +96,10 @@ SIGNATURES = {
     "rt_device_count": (C.c_int, []),
     "rt_last_error": (C.c_char_p, []),
     "rt_version": (C.c_char_p, []),
+    "rt_abi_version": (C.c_int, []),
 }
+
+RT_ABI_VERSION = 3   # include/rt.h; the structures above are this revision's
 
 
 def load(path: Path) -> C.CDLL:
@@ -109,6 +114,9 @@ def load(path: Path) -> C.CDLL:
         fn = getattr(dll, name)
         fn.restype = res
         fn.argtypes = args
+    if dll.rt_abi_version() != RT_ABI_VERSION:
+        raise ImportError(f"{path}: ABI revision {dll.rt_abi_version()}, this binding is {RT_ABI_VERSION} "
+                          "(rebuild the library: make -C raytracing-clj_amd)")
     return dll
 
 

@@ -52,7 +52,18 @@ def test_struct_layouts_match_header():
     assert C.sizeof(rt_camera) == 18 * 4 + 4
     assert C.sizeof(rt_scene) == 32
     assert rt_params.seed.offset == 24 and C.sizeof(rt_params) == 56
-    assert C.sizeof(rt_stats) == 64 and rt_stats.upload_ms.offset == 40
+    assert C.sizeof(rt_stats) == 112 and rt_stats.upload_ms.offset == 40 and rt_stats.d2h_ms.offset == 104
+
+
+def test_abi_revision_matches_header():
+    """rt.h's RT_ABI_VERSION == the binding's == the loaded library's
+    (rt_stats grew without a revision the caller could check)."""
+    import rtclj
+    from rtclj._lib import RT_ABI_VERSION
+    hdr = (ROOT / "include" / "rt.h").read_text()
+    m = re.search(r"#define RT_ABI_VERSION (\d+)", hdr)
+    assert m and int(m.group(1)) == RT_ABI_VERSION == rtclj.lib.rt_abi_version()
+    assert f"abi {RT_ABI_VERSION}" in rtclj.lib.rt_version().decode()
 
 
 def test_no_gpu_here_fails_loudly():

@@ -1,0 +1,92 @@
+"""The non-Python host of the C ABI on the GPU: lib/rt_main, the C++ driver
+that mirrors `clojure -M:main [spp] [depth]` (src/raytracing.clj:95-177) and
+`clojure -M:realm` (src/realm/raytracing.clj:279-359), run as a fresh child
+process.  Unlike the pytest process (torch's bundled HIP runtime, loaded first
+by conftest.gpu_lib), the child loads /opt/rocm's libamdhip64 through
+librtclj.so's own dependency -- the runtime a JVM or C++ host gets.
+
+Its scene.ppm must equal write-color! (rt_quantize) of the oracle's fp32
+kernel mirror at the same seed, byte for byte; the PNG it writes decodes to
+the same pixels.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+RT_MAIN = ROOT / "raytracing-clj_amd" / "lib" / "rt_main"
+
+
+def _child_env():
+    env = dict(os.environ)
+    env.pop("RTCLJ_LIBRARY", None)
+    return env
+
+
+def _run(args, tmp_path):
+    assert RT_MAIN.exists(), "lib/rt_main is not built (make -C raytracing-clj_amd)"
+    r = subprocess.run([str(RT_MAIN), *args], cwd=tmp_path, capture_output=True, text=True, timeout=120,
+                       env=_child_env())
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    return r.stdout
+
+
+def _mirror_q8(mode, scene, cam, w, h, spp, depth, seed):
+    from rtclj import raytracing as R
+    out, _, segs, smp = oracle.render(mode, scene.sphere.astype(np.float64), scene.kind,
+                                      scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
+                                      seed=seed, nthreads=min(16, os.cpu_count() or 1))
+    return R.write_color(out), segs / smp
+
+
+def _segs_per_sample(stdout):
+    line = [ln for ln in stdout.splitlines() if "segments/sample" in ln][-1]
+    return float(line.split(",")[-1].split()[0])
+
+
+def test_rt_main_reference_scene_equals_mirror(gpu_lib, tmp_path):
+    from pngdec import decode
+    from rtclj import raytracing as R
+    out = _run(["16", "50", "--out", "scene.ppm", "--png", "scene.png", "--gpus", "1"], tmp_path)
+    assert out.startswith("config: {:samples-per-px 16, :max-depth 50}")
+    img = R.read_ppm(tmp_path / "scene.ppm")
+    assert img.shape == (225, 400, 3)
+    sc = R.Scene.from_bodies(R.hittables)
+    cam = R.camera(400, 225, **R.REFERENCE_CAMERA)
+    ref, sps = _mirror_q8(oracle.MODE_MIRROR32, sc, cam, 400, 225, 16, 50, seed=1)
+    assert np.array_equal(img, ref)
+    assert abs(_segs_per_sample(out) - sps) < 1e-3
+    assert np.array_equal(decode((tmp_path / "scene.png").read_bytes())[0], img)
+
+
+def test_rt_main_realm_equals_mirror(gpu_lib, tmp_path):
+    from rtclj import raytracing as R
+    from rtclj import realm
+    _run(["8", "50", "--realm", "--out", "realm.ppm"], tmp_path)
+    img = R.read_ppm(tmp_path / "realm.ppm")
+    w, h = 400, realm.image_height(400)
+    assert img.shape == (h, w, 3) == (224, 400, 3)
+    sc = R.Scene.from_bodies(realm.hittables)
+    ref, _ = _mirror_q8(oracle.MODE_REALM32, sc, realm.camera(w, h), w, h, 8, 50, seed=1)
+    assert np.array_equal(img, ref)
+
+
+def test_rt_main_cover_scene(gpu_lib, tmp_path):
+    """The benchmark scene (cover, 484 bodies: the BVH traversal) through the
+    C++ host at another width and seed."""
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    _run(["4", "50", "--scene", "cover", "--width", "160", "--seed", "9", "--out", "c.ppm"], tmp_path)
+    img = R.read_ppm(tmp_path / "c.ppm")
+    h = R.image_height(160)
+    ref, _ = _mirror_q8(oracle.MODE_MIRROR32, scenes.cover(11), scenes.cover_camera(160, h), 160, h, 4, 50, seed=9)
+    assert np.array_equal(img, ref)
