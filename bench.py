@@ -48,7 +48,7 @@ import torch.distributed as dist  # noqa: E402
 import rtclj  # noqa: E402
 from rtclj import raytracing as R  # noqa: E402
 from rtclj import scenes  # noqa: E402
-from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0, check, diag_lib, lib, rt_params  # noqa: E402
+from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0, RT_FLAG_STREAMED, check, diag_lib, lib, rt_params  # noqa: E402
 from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
 # BASELINE.json's metric is quoted on C1; the other workloads report the same
@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant; 0 = default)")
     ap.add_argument("--schedule", type=int, default=0,
                     help="tile schedule (rt_set_schedule): 0 adaptive longest-first, 1 plain dispatch order")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: consecutive frames go round-robin to this many streams "
+                         "(rt_launch RT_FLAG_STREAMED when > 1); 1 = one stream, one frame at a time")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -416,14 +419,25 @@ def main():
     p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
     rows = check(lib.rt_rows_out(C.byref(p)))
     assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
-    out = torch.empty(rows * W * 3, dtype=torch.float32, device=dev)
+    # frames in flight: frame k on streams[k % inflight], each stream its own
+    # output buffer (and, in the library, its own tile-order record and split
+    # sums); the frames are independent, so frame k+1's workgroups take the
+    # slots frame k's tail frees
+    inflight = max(1, a.inflight)
+    ps = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
+    if inflight > 1:
+        ps.flags |= RT_FLAG_STREAMED
+    streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
+    outs = [torch.empty(rows * W * 3, dtype=torch.float32, device=dev) for _ in range(inflight)]
+    out = outs[0]
     counters = torch.zeros(2, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = streams[0]
     sh = C.c_void_p(stream.cuda_stream)
+    shs = [C.c_void_p(x.cuda_stream) for x in streams]
 
-    def step():
-        check(lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()),
-                            C.c_void_p(counters.data_ptr()), sh))
+    def step(k=0, params=ps):
+        check(lib.rt_launch(ds, C.byref(cam), C.byref(params), C.c_void_p(outs[k % inflight].data_ptr()),
+                            C.c_void_p(counters.data_ptr()), shs[k % inflight]))
 
     def barrier():
         if world > 1:
@@ -436,15 +450,29 @@ def main():
     if a.warmup > 0 and a.schedule == 0:
         f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         check(lib.rt_set_schedule(1))
-        step()
+        step(0, p)
         f0.record(stream)
-        step()
+        step(0, p)
         f1.record(stream)
         torch.cuda.synchronize()
         first_ms = f0.elapsed_time(f1)
         check(lib.rt_set_schedule(a.schedule))
-    for _ in range(a.warmup):
-        step()
+    # one frame at a time on one stream (no RT_FLAG_STREAMED): the kernel's
+    # own duration, which the roofline and the rocprof average use
+    single_ms = None
+    if a.warmup > 0:
+        for _ in range(2):
+            step(0, p)
+        n1 = max(3, min(20, a.steps))
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n1)]
+        for e0, e1 in ev:
+            e0.record(stream)
+            step(0, p)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        single_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / n1
+    for k in range(a.warmup * inflight):
+        step(k)
     torch.cuda.synchronize()
     counters.zero_()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
@@ -453,9 +481,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        starts[k].record(stream)
-        step()
-        ends[k].record(stream)
+        s_k = streams[k % inflight]
+        starts[k].record(s_k)
+        step(k)
+        ends[k].record(s_k)
     torch.cuda.synchronize()
     # each rank's own steps, from the common barrier to its last kernel's end;
     # the max over ranks below is the job's time (the closing barrier itself,
@@ -466,9 +495,10 @@ def main():
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     cnt = counters.to("cpu").tolist()
     mine = {"rank": rank, "device": device, "elapsed_s": elapsed, "elapsed_barrier_s": time.perf_counter() - t0,
-            "kernel_ms_avg": sum(kern_ms) / len(kern_ms),
+            "kernel_ms_avg": single_ms if single_ms is not None else sum(kern_ms) / len(kern_ms),
+            "launch_span_ms_avg": sum(kern_ms) / len(kern_ms),
             "kernel_ms_max": max(kern_ms), "rows": rows, "segments": cnt[0], "samples": cnt[1],
-            "first_launch_ms": first_ms}
+            "first_launch_ms": first_ms, "ms_per_frame": elapsed / a.steps * 1e3}
     per_rank = [mine]
     if world > 1:
         per_rank = [None] * world
@@ -534,13 +564,22 @@ def main():
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB written once) + "
                                      "bodies*32 (scene read); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch"},
             "valu": valu, "occupancy": occ, "stats_build": stats,
-            "kernel_ms_avg": kern_avg_ms, "kernel_ms_max": mine["kernel_ms_max"],
+            "kernel_ms_avg": kern_avg_ms, "launch_span_ms_max": mine["kernel_ms_max"],
             "dispatch_order": {"kernel_ms": mine["first_launch_ms"],
                                "note": "the same frame with tiles in plain dispatch order (rt_set_schedule(1)), as a "
                                        "launch of a new shape runs (no tile costs yet); the timed steps dispatch "
                                        "longest first by the previous launches' per-tile durations (each added to half the record before it)"},
+            "frames_in_flight": {"streams": inflight, "rt_launch_flags": "RT_FLAG_STREAMED" if inflight > 1 else 0,
+                                 "launch_span_ms_avg": mine["launch_span_ms_avg"],
+                                 "note": "timed frames go round-robin to this many streams (independent frames: "
+                                         "the next frame's workgroups take the slots this frame's tail frees); "
+                                         "kernel_ms_avg and the roofline are the same frame launched alone on one "
+                                         "stream; launch_span_ms_avg = each timed frame's start-to-end on its stream "
+                                         "(spans overlap)"},
             "per_rank": {"kernel_ms_avg": kms, "rows": [r["rows"] for r in per_rank],
-                         "imbalance": max(kms) / (sum(kms) / len(kms)),
+                         "ms_per_frame": [r["ms_per_frame"] for r in per_rank],
+                         "imbalance": max(r["ms_per_frame"] for r in per_rank) /
+                                      (sum(r["ms_per_frame"] for r in per_rank) / len(per_rank)),
                          "elapsed_ms": [r["elapsed_s"] * 1e3 for r in per_rank],
                          "elapsed_with_closing_barrier_ms": max(r["elapsed_barrier_s"] for r in per_rank) * 1e3},
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_total / a.steps,

@@ -110,7 +110,8 @@ typedef struct rt_params {
   int row_tile;           /* interleaved tile height (rows); 0 -> 8            */
   int tile_first;         /* rt_launch: first tile of this shard               */
   int tile_step;          /* rt_launch: tile stride (0 = contiguous rows)      */
-  int flags;              /* 0, RT_FLAG_REALM, RT_FLAG_SHARDS_ON_DEVICE0 (ored) */
+  int flags;              /* 0, RT_FLAG_REALM, RT_FLAG_SHARDS_ON_DEVICE0 (rt_render),
+                             RT_FLAG_STREAMED (rt_launch), ored                 */
 } rt_params;
 
 /* rt_render: split into n_devices interleaved-tile shards exactly as for n
@@ -126,6 +127,15 @@ typedef struct rt_params {
  * camera (no defocus, focal length |lookfrom - lookat|) is an rt_camera like
  * any other (rt_camera_setup with defocus_angle 0). */
 #define RT_FLAG_REALM 2
+
+/* rt_launch only: the caller keeps launches of consecutive frames in flight
+ * on two (or more) streams of the device, so the next frame's workgroups fill
+ * the slots this launch's tail frees.  A launch of few tiles then splits its
+ * tiles' samples for two rounds of workgroups instead of three (fewer, longer
+ * sample pools: each pool's end idles lanes; the tail no longer waits alone).
+ * Timing only: the bits never depend on it.  (tools/shard_time.py
+ * --inflight; bench.py's frames in flight) */
+#define RT_FLAG_STREAMED 4
 
 /* ---- per-call statistics (device-side counters, host timers) ------------ */
 typedef struct rt_stats {

@@ -1774,7 +1774,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
                          uint64_t* d_counters, void* hip_stream) {
   clear_error();
   if (!ds || !c || !p || !d_out) return set_error(RT_E_ARG, "rt_launch: NULL argument");
-  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP || (p->flags & ~RT_FLAG_REALM) != 0)
+  if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP ||
+      (p->flags & ~(RT_FLAG_REALM | RT_FLAG_STREAMED)) != 0)
     return set_error(RT_E_ARG, "rt_launch: bad width/height/spp/flags");
   const int rows = rows_out(*p);
   if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
@@ -1872,7 +1873,15 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     } else {
       const int slots = launch_slots(ds->device, v.fn, lds);
       const int64_t want = static_cast<int64_t>(kSplitRounds) * slots;
-      if (slots > 0 && n_tiles < want) split = static_cast<int>((want + n_tiles - 1) / n_tiles);
+      if (slots > 0 && n_tiles < want) {
+        split = static_cast<int>((want + n_tiles - 1) / n_tiles);
+        // frames in flight: the next frame fills this launch's tail, so two
+        // rounds of workgroups suffice (at least 2 splits: an unsplit heavy
+        // tile would outlive two frames).  C1's 8-GPU shard, 2 streams:
+        // 0.817 ms per frame at split 2 vs 0.87 at 3 (profiles/r03/shard_matrix_*.txt)
+        if (p->flags & RT_FLAG_STREAMED)
+          split = std::max(2, static_cast<int>((2 * static_cast<int64_t>(slots) + n_tiles - 1) / n_tiles));
+      }
     }
     split = std::min(split, std::min(p->spp, kSplitMax));
     if (split > 1) n_whole = 0;

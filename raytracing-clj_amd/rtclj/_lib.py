@@ -22,6 +22,7 @@ RT_MAX_SPHERES = 8192
 RT_MAX_SPP = 1 << 24
 RT_FLAG_SHARDS_ON_DEVICE0 = 1
 RT_FLAG_REALM = 2
+RT_FLAG_STREAMED = 4
 
 
 class RTError(RuntimeError):

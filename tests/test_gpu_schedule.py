@@ -228,3 +228,44 @@ def test_sample_split_shards_realm_and_stripes(env, split_env):
             assert np.array_equal(part, full[rows]), (k, f)
         assert np.array_equal(_launch(env, cam, w, h, 5, sample_begin=7), stripe), k
         assert np.array_equal(_render(sc, cam, w, h, 6, flags=RT_FLAG_REALM), realm), k
+
+
+def test_streamed_frames_in_flight_are_bit_exact(env):
+    """RT_FLAG_STREAMED (include/rt.h): C1's 8-GPU shard and 4-GPU shard
+    launched as frames in flight -- round-robin over two streams, each stream
+    its own output buffer, tile-order record and split sums, never
+    synchronised in between -- equal rt_render's rows of the same frame, every
+    frame.  The flag changes the sample split (two rounds of workgroups, at
+    least 2 splits), never a bit."""
+    from rtclj import scenes
+    from rtclj._lib import RT_FLAG_STREAMED, check, lib, rt_params
+    from rtclj.shard import shard_params, shard_rows
+    sc, ds, torch = env
+    w, h, spp = 1200, 675, 24
+    cam = scenes.cover_camera(w, h)
+    full = _render(sc, cam, w, h, spp)
+    for world in (8, 4):
+        rank = world - 1
+        p = rt_params(**shard_params(world, rank, w, h, spp, 50, 1, "strong"))
+        p.flags |= RT_FLAG_STREAMED
+        n = check(lib.rt_rows_out(C.byref(p)))
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        frames = []
+        for f in range(6):
+            s = streams[f % 2]
+            with torch.cuda.stream(s):
+                out = torch.full((n * w * 3,), float("nan"), dtype=torch.float32, device="cuda")
+            rc = lib.rt_launch(ds, C.byref(cam), C.byref(p), C.c_void_p(out.data_ptr()), None,
+                               C.c_void_p(s.cuda_stream))
+            assert rc == 0, lib.rt_last_error()
+            frames.append(out)
+        torch.cuda.synchronize()
+        want = full[shard_rows(h, 8, rank, world)]
+        for f, out in enumerate(frames):
+            got = out.cpu().numpy().reshape(n, w, 3)
+            assert np.array_equal(got, want), (world, f)
+    # rt_render is one frame per call: the flag is rt_launch's only
+    from rtclj import raytracing as R
+    from rtclj._lib import RTError
+    with pytest.raises(RTError):
+        R.render(sc, cam, 64, 36, spp=2, flags=RT_FLAG_STREAMED)

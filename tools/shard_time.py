@@ -7,6 +7,11 @@ then --reps timed launches): the max over ranks predicts the N-GPU step time
 that bench.py --gpus N measures, without an N-GPU node.
 
   python tools/shard_time.py [--workload c1] [--worlds 1 2 4 8] [--reps 5]
+                             [--inflight S --frames F]
+
+--inflight S: also time F back-to-back frames of each rank's shard issued
+round-robin over S streams (frames in flight: frame k+1's workgroups fill the
+slots frame k's tail frees), per-frame time = total / F.
 """
 import argparse
 import ctypes as C
@@ -22,7 +27,7 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 
 from rtclj import raytracing as R, scenes  # noqa: E402
-from rtclj._lib import check, lib, rt_params  # noqa: E402
+from rtclj._lib import RT_FLAG_STREAMED, check, lib, rt_params  # noqa: E402
 from rtclj.shard import shard_params  # noqa: E402
 from bench import WORKLOADS  # noqa: E402
 
@@ -34,6 +39,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--row-tile", type=int, default=8, help="rows per interleaved shard tile")
+    ap.add_argument("--inflight", type=int, nargs="+", default=[0],
+                    help="stream counts for the pipelined measurement (0: off)")
+    ap.add_argument("--frames", type=int, default=40)
+    ap.add_argument("--no-streamed-flag", action="store_true",
+                    help="pipelined launches without RT_FLAG_STREAMED (the single-frame split policy)")
     ap.add_argument("--configs", nargs="*", default=[""],
                     help="environment settings per measurement, e.g. RTCLJ_SPLIT=4,RTCLJ_RING=2 ('' = defaults)")
     a = ap.parse_args()
@@ -63,8 +73,9 @@ def main():
 def run(a, wl, W, H, spp, sc, cam, sh, stream):
     res = {"workload": a.workload, "spp": spp, "worlds": {}}
     t1 = None
+    t1p = {}
     for n in a.worlds:
-        per = []
+        per, per_pipe = [], {}
         for r in range(n):
             ds = C.c_void_p()
             check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
@@ -87,13 +98,45 @@ def run(a, wl, W, H, spp, sc, cam, sh, stream):
                 torch.cuda.synchronize()
                 ts.append(s.elapsed_time(e))
             per.append(statistics.median(ts))
+            for nin in a.inflight:
+                if nin <= 0:
+                    continue
+                streams = [torch.cuda.Stream() for _ in range(nin)]
+                outs = [torch.empty_like(out) for _ in streams]
+                shs = [C.c_void_p(x.cuda_stream) for x in streams]
+                pp = rt_params(**shard_params(n, r, W, H, spp, wl["depth"], 1, "strong", row_tile=a.row_tile))
+                if not a.no_streamed_flag:
+                    pp.flags |= RT_FLAG_STREAMED
+
+                def launch_on(i):
+                    check(lib.rt_launch(ds, C.byref(cam), C.byref(pp), C.c_void_p(outs[i].data_ptr()),
+                                        C.c_void_p(cnt.data_ptr()), shs[i]))
+                for _ in range(2):   # each stream's own schedule record
+                    for i in range(nin):
+                        launch_on(i)
+                torch.cuda.synchronize()
+                import time
+                t0 = time.perf_counter()
+                for f in range(a.frames):
+                    launch_on(f % nin)
+                torch.cuda.synchronize()
+                per_pipe.setdefault(nin, []).append((time.perf_counter() - t0) * 1e3 / a.frames)
             lib.rt_scene_free(ds)
         mx = max(per)
         if n == 1:
             t1 = mx
         res["worlds"][n] = {"max_ms": mx, "mean_ms": sum(per) / n, "per_rank_ms": per,
                             "speedup": (t1 / mx) if t1 else None}
-        print(f"N={n}: max {mx:.3f} ms mean {sum(per) / n:.3f} ms speedup {t1 / mx if t1 else 0:.2f}", flush=True)
+        msg = f"N={n}: max {mx:.3f} ms mean {sum(per) / n:.3f} ms speedup {t1 / mx if t1 else 0:.2f}"
+        for nin, pp in per_pipe.items():
+            pm = max(pp)
+            if n == 1:
+                t1p[nin] = pm
+            res["worlds"][n][f"pipelined_{nin}"] = {"max_ms": pm, "per_rank_ms": pp,
+                                                     "speedup_vs_1gpu_pipelined": t1p[nin] / pm,
+                                                     "speedup_vs_1gpu_single": t1 / pm}
+            msg += (f" | {nin} streams: {pm:.3f} ms/frame x{t1p[nin] / pm:.2f} (vs 1-GPU single x{t1 / pm:.2f})")
+        print(msg, flush=True)
     return res
 
 
