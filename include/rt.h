@@ -311,6 +311,13 @@ int rt_debug_stats(uint64_t* out32);
  * the count. */
 int rt_debug_waves(int device, uint64_t* out, size_t n_waves);
 
+/* Sample stealing of rt_launch (diagnostic): the launches on (ds, hip_stream)
+ * since the last call made out2[0] steals of out2[1] samples in all (a
+ * workgroup that finds no tile left to start takes free samples of another
+ * workgroup's tile).  Waits for the stream, then clears the
+ * counts.  Timing only: the bits never depend on it. */
+int rt_steal_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2);
+
 int rt_device_count(void);
 const char* rt_last_error(void);
 const char* rt_version(void);

@@ -96,6 +96,30 @@ struct alignas(16) KArgs {
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
   uint32_t key;
+  // Tile sharing.  Workgroups [0, n_units) run the units
+  // (dispatch positions); the grid's last workgroups are helpers,
+  // dispatched once every unit has been, i.e. into the launch's tail.  The
+  // sample pool [0, P) of a published whole tile is handed out from
+  // word[tile] = (epoch << 48) | (helpers << 32) | next (epoch: the
+  // launch's, 16 bits, so that a word left by an earlier launch on the
+  // stream is never taken for this one's; the owner entries are cleared
+  // when it wraps): every wave of its owner and of each
+  // helper that joins it claims batches of kShareBatch samples until the
+  // pool is spent, so they finish together.  Owners publish their tile in owner[unit %
+  // n_owner]; a helper looks at a window of those and joins the tile with
+  // the most unclaimed samples (at least steal_min).  A shared tile's pixel
+  // sums meet in sum[tile] (u64 atomics, zero between uses); whoever brings
+  // done[tile] to P converts them.  word NULL: no sharing.
+  unsigned long long* word;      // per tile
+  unsigned* done;                // per tile
+  unsigned long long* sum;       // per tile: NPX x 3
+  int* owner;                    // n_owner: tiles being run (-1: none)
+  unsigned long long* stealc;    // [helpers that got samples, samples they claimed] (rt_steal_stats)
+  int n_owner;
+  int n_units;
+  int steal_min;
+  int batch_max;                 // a wave's largest claim on a shared tile
+  unsigned epoch;                // this launch's (per stream, 1 .. 65535)
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -202,6 +226,46 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+// Cross-workgroup words of the stealing protocol: only
+// ever touched by agent-scope atomics (read-modify-write, executed coherently
+// for every XCD; a plain or sc1 load could hit a stale line in the reader's
+// XCD L2), and a returned value is waited on before the next one is issued.
+__device__ __forceinline__ unsigned long long xread64(unsigned long long* p) {
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int xread32(int* p) {
+  return __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool xcas64(unsigned long long* p, unsigned long long& expect, unsigned long long v) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+// a wave's smallest claim on a shared tile (2 samples per lane: fixed
+// batches of 64 cost 1 % at one GPU, of 256 lose the balance at the tail;
+// profiles/r03/share_ab.txt)
+constexpr int kShareBatch = 128;
+__device__ __forceinline__ unsigned word_epoch(unsigned long long w) { return static_cast<unsigned>(w >> 48); }
+__device__ __forceinline__ int word_helpers(unsigned long long w) { return static_cast<int>((w >> 32) & 0xffffu); }
+// a workgroup-uniform value read from LDS, moved to a scalar register (an LDS
+// read lands in a VGPR, and everything derived from it would stay there)
+__device__ __forceinline__ int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long sgpr64(unsigned long long v) {
+  return (static_cast<unsigned long long>(static_cast<unsigned>(sgpr(static_cast<int>(v >> 32)))) << 32) |
+         static_cast<unsigned>(sgpr(static_cast<int>(v)));
+}
+
+// A pointer to the kernel's arguments the compiler cannot see through: the
+// loads made through it stay where they are written.  The unit loop reads its
+// set-up and epilogue arguments this way, so they are re-loaded per unit
+// instead of being hoisted out of the loop and kept live in SGPRs across the
+// hot loop (which spilled SGPRs into VGPR lanes: 76 -> 102 VGPRs).
+typedef const struct KArgs __attribute__((address_space(4)))* KArgsP;
+__device__ __forceinline__ KArgsP kargs_opaque() {
+  KArgsP p = (KArgsP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
 enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4, SCAN_BVHQ = 5, SCAN_BVHO = 6 };
@@ -236,15 +300,34 @@ constexpr int kTile = 8;
 constexpr int kPoolPx = kTile * kTile;
 constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : kTile; }
 
+// Waves per SIMD the register allocator must leave room for: six for the
+// default traversal (80 VGPRs; its 26.5 KB LDS image fits 6 workgroups per
+// CU), five for the 8-body-leaf one (C4: its LDS allows 5 workgroups per
+// CU).  Without the bound the unit loop's longer-lived uniform values
+// (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
+// waves; with it, a few of them spill to scratch outside the hot loop.
+constexpr int min_waves(int scan, bool stats) { return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHO ? 5 : 1; }
+
 template <int SRC, int SCAN, bool STATS = false>
-__global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
+__global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(const KArgs a) {
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
   // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample
   // j / npx: the lanes ending paths together add into different pixels'
   // sums).  A lane whose path ends takes the next index from an LDS counter
   // (one ds_add per wave event, then an mbcnt prefix).  The colour sums are
   // u64 per pixel and channel in LDS, added with ds_add_u64: order-free.
+  //
+  // The workgroup's unit: a whole tile (owner) or one sample split of a
+  // tile, or -- a helper -- a share of another workgroup's tile (DESIGN.md
+  // §3.1).  Each wave runs its samples from a batch of consecutive pool
+  // indices it claimed: from s_pool_next, or for a shared tile from the
+  // tile's word.
   __shared__ int s_pool_next;
+  __shared__ int s_cnt;               // samples this workgroup claimed (shared tiles)
+  __shared__ int s_join;              // helpers the owner's claims saw (> 0: the tile was shared)
+  __shared__ int s_unit[2];           // a helper's tile and first index
+  __shared__ unsigned long long s_best;
+  __shared__ int s_last;
   // A/B build only (-DRTCLJ_AB_RING): camera samples made in
   // per-wave batches into LDS rings.  Worth 2.6 % at 5 workgroups per CU,
   // but its 5 KB of LDS keep the default traversal from the sixth (§8)
@@ -269,8 +352,70 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) float4 s_geo[];
   const int n = a.n;
-  if (threadIdx.x == 0) s_pool_next = kRing ? 0 : 256;   // (the ring claims its own)
-  if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
+  const int lane = threadIdx.x & 63;
+  const int unit = static_cast<int>(blockIdx.x);
+  // (set-up and epilogue arguments through an opaque pointer: re-loaded
+  // where used, not kept in SGPRs across the hot loop)
+  const KArgsP ka = kargs_opaque();
+  const bool own = unit < ka->n_units;
+  // samples of whole tile t (its in-image pixels x spp)
+  auto tile_pool = [&](KArgsP kp, int t) {
+    const int ty = t / kp->tiles_x, tx = t - ty * kp->tiles_x;
+    const int w = max(0, min(kTile, kp->width - tx * kTile)), h = max(0, min(TH, kp->rows_out - ty * TH));
+    return kp->spp > 0 && kp->max_depth > 0 ? w * h * kp->spp : 0;
+  };
+  if (!own) {
+    // ---- a helper: pick a tile still running, join it ----
+    if (kRing || !ka->word) return;
+    if (threadIdx.x == 0) {
+      s_best = 0ull;
+      s_unit[0] = -1;
+    }
+    __syncthreads();
+    // each thread looks at 2 owner entries of a window of 512 that starts at
+    // a per-helper offset (atomic reads: entries change as owners start
+    // tiles); key = (unclaimed << 32) | tile, the most unclaimed wins
+    const int M = ka->n_owner;
+    const int w0 = static_cast<int>(mix32(static_cast<uint32_t>(unit)) % static_cast<uint32_t>(M));
+    unsigned long long key = 0;
+    for (int i = 0; i < 2; ++i) {
+      int w = w0 + static_cast<int>(threadIdx.x) + 256 * i;
+      w = w >= M ? w - M : w;
+      w = w >= M ? w % M : w;
+      const int t = xread32(&ka->owner[w]);
+      if (t >= 0) {
+        const unsigned long long wd = xread64(&ka->word[t]);
+        const int fr = word_epoch(wd) == ka->epoch ? tile_pool(ka, t) - static_cast<int>(static_cast<unsigned>(wd)) : 0;
+        const unsigned long long k2 = (static_cast<unsigned long long>(fr) << 32) | static_cast<unsigned>(t);
+        key = (fr >= ka->steal_min && k2 > key) ? k2 : key;
+      }
+    }
+    key = wave_max_u64(key);
+    if (lane == 0 && key) __hip_atomic_fetch_max(&s_best, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    const unsigned long long best_key = sgpr64(s_best);
+    if (best_key == 0) return;   // nothing worth joining in the window
+    if (threadIdx.x == 0) {
+      // join: one atomic counts the helper in and claims its lanes' first indices
+      const int t = static_cast<int>(static_cast<unsigned>(best_key));
+      const int P = tile_pool(ka, t);
+      const unsigned long long wd = __hip_atomic_fetch_add(&ka->word[t], (1ull << 32) + 256u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+      const int g = static_cast<int>(static_cast<unsigned>(wd));
+      if (word_epoch(wd) == ka->epoch && g < P) {   // (another epoch: a spent word of an earlier launch)
+        const int got = min(P - g, 256);
+        __hip_atomic_fetch_add(&ka->stealc[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&ka->stealc[1], static_cast<unsigned long long>(got), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        s_unit[0] = t;
+        s_unit[1] = g;
+        s_cnt = got;
+      }
+    }
+    __syncthreads();
+    if (sgpr(s_unit[0]) < 0) return;   // spent meanwhile
+  }
+  // the scene image (a thief only once it has samples to run)
   if constexpr (SRC == SRC_LDS) {
     if constexpr (is_bvh_scan(SCAN)) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
@@ -279,33 +424,39 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
     }
   }
-  __syncthreads();
+  uint32_t segs = 0;
+  if (STATS || ka->tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
   // BVH traversal stack: bvh_stack node refs per lane, [entry][lane] (no bank conflicts)
   // (u8 entries for the 8-body-leaf traversal, whose trees the host caps at
   // 256 nodes: with its u16 body indices this keeps a 1000-body scene's
   // image under the 32 KB that 5 workgroups per CU allow)
   using StackT = std::conditional_t<SCAN == SCAN_BVHO, unsigned char, unsigned short>;
   StackT* s_stack = reinterpret_cast<StackT*>(
-      reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? a.bvh_blob_f4 * 16 : 0));
+      reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? ka->bvh_blob_f4 * 16 : 0));
 
-  const int lane = threadIdx.x & 63;
-  // the block's unit: a whole tile (dispatch slots [0, n_whole)) or one
-  // sample split of a tile at the order's end
-  const int slot = static_cast<int>(blockIdx.x);
-  int pos = slot, split_ix = 0;
-  const bool split = slot >= a.n_whole;
-  if (split) {
-    const int v = slot - a.n_whole;
-    const int t = v / a.split;
-    pos = a.n_whole + t;
-    split_ix = v - t * a.split;
+  // the unit: a whole tile or one sample split of a tile at the order's end
+  // (own), or a stolen sample range [first, s_lim) of a whole tile
+  int tile, split_ix = 0, first = 0;
+  bool split = false;
+  if (own) {
+    int pos = unit;
+    split = unit >= ka->n_whole;
+    if (split) {
+      const int v = unit - ka->n_whole;
+      const int t = v / ka->split;
+      pos = ka->n_whole + t;
+      split_ix = v - t * ka->split;
+    }
+    tile = ka->tile_order ? ka->tile_order[pos] : pos;
+  } else {
+    tile = sgpr(s_unit[0]);
+    first = sgpr(s_unit[1]);
   }
-  const int tile = a.tile_order ? a.tile_order[pos] : pos;
-  const int tby = tile / a.tiles_x, tbx = tile - tby * a.tiles_x;
+  const int tby = tile / ka->tiles_x, tbx = tile - tby * ka->tiles_x;
   // the tile's in-image part, vw x vh pixels; pool pixel q at (q % vw, q / vw)
   const int qx0 = tbx * kTile, qy0 = tby * TH;
-  const int vw = max(0, min(kTile, a.width - qx0));
-  const int vh = max(0, min(TH, a.rows_out - qy0));
+  const int vw = max(0, min(kTile, ka->width - qx0));
+  const int vh = max(0, min(TH, ka->rows_out - qy0));
   const int npx = vw * vh;
 
   // compacted output row -> global image row (interleaved row tiles)
@@ -320,17 +471,38 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     return mix32(a.key ^ mix32(static_cast<uint32_t>(y) * static_cast<uint32_t>(a.width) + static_cast<uint32_t>(x)));
   };
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
-  uint32_t segs = 0;
 
   // the unit's samples [k0, k0 + cnt) of each pixel
-  const int k0 = split ? a.split_k0[split_ix] : 0;
-  const int cnt = split ? a.split_k0[split_ix + 1] - k0 : a.spp;
+  const int k0 = split ? ka->split_k0[split_ix] : 0;
+  const int cnt = split ? ka->split_k0[split_ix + 1] - k0 : ka->spp;
   // pool index j -> (pixel q = j % npx, sample k0 + j / npx); the next free
   // index is `base`.  j / npx by a 64-bit magic (exact for every 32-bit j);
   // q / vw by multiply-high (exact: q < 64, vw <= 8)
-  const int pool = (cnt > 0 && a.max_depth > 0) ? npx * cnt : 0;
+  const int pool = (cnt > 0 && ka->max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
+  // the unit's LDS state.  The owner of a whole tile of more than 512
+  // samples shares it: the tile's word with this launch's epoch, its lanes'
+  // first 256 indices claimed and no helper, then its owner entry.  (No
+  // order is needed between the two: a helper that reads the word before it
+  // lands sees another epoch and leaves it alone.  done[tile] is 0 already:
+  // zeroed at allocation and by the workgroup that completes a shared tile.)
+  const bool shared_tile = !kRing && ka->word && !split && (!own || pool > 512);
+  // where the waves claim their batches: the shared tile's word, else (NULL)
+  // the workgroup's s_pool_next
+  unsigned long long* const src = shared_tile ? ka->word + tile : nullptr;
+  const int kc_batch_max = ka->batch_max;
+  if (threadIdx.x == 0) {
+    if (own && shared_tile) {
+      __hip_atomic_exchange(&ka->word[tile], (static_cast<unsigned long long>(ka->epoch) << 48) | 256ull,
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_exchange(&ka->owner[unit % ka->n_owner], tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_cnt = 256;
+    }
+    s_join = own ? 0 : 1;
+    s_pool_next = kRing ? 0 : 256;   // (the ring claims its own)
+  }
+  if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
@@ -345,9 +517,12 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       const int gy = image_row(qy0 + qy);
       s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
     }
-    __syncthreads();
   }
-  int j = static_cast<int>(threadIdx.x), base = 0, q = 0, k = 0;
+  __syncthreads();
+  // the wave's batch [wb, we) of pool indices (wave-uniform; empty at first:
+  // the lanes start on first + threadIdx.x)
+  int wb = 0, we = 0;
+  int j = first + static_cast<int>(threadIdx.x), q = 0, k = 0;
   bool active = kRing ? true : j < pool;
 
   // path state
@@ -1128,21 +1303,54 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
       __hip_atomic_fetch_add(acc + 2, static_cast<unsigned long long>(fix24(cb)), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // refill: one LDS atomic per wave event hands out the next popc(m) indices
+    // refill: the lanes whose paths ended take their next indices
     const uint64_t m = __ballot(done);
     if constexpr (kRing) {
       if (m) ring_take(m, done);
     } else if (m) {
-      const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
-      int old = 0;
-      if (lane == leader) old = atomicAdd(&s_pool_next, static_cast<int>(__popcll(m)));
-      base = __builtin_amdgcn_readlane(old, leader);
-    }
-    if (!kRing && done) {
-      j = base + static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
-      fresh = true;
-      if (j >= pool) active = false;
+      // the lanes in m take the next indices of the wave's batch, in rank
+      // order; when it runs out the wave claims another: 64 indices from
+      // s_pool_next, or for a shared tile 128-1024 from the tile's word
+      // (whose helper count tells the owner whether the tile was shared).
+      // A claim past the pool leaves the remaining lanes without one: they
+      // retire, and every later claim of the wave would be past it too.
+      const int need = static_cast<int>(__popcll(m));
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+      int nj = -1;
+      for (int r0 = 0;;) {
+        const int take = min(we - wb, need - r0);
+        if (rank >= r0 && rank < r0 + take) nj = wb + (rank - r0);
+        wb += take;
+        r0 += take;
+        if (r0 >= need || we >= pool) break;
+        int g = 0;
+        // a shared tile's claims shrink as its pool is spent (guided: an
+        // eighth of what is left past this wave's last batch, kShareBatch ..
+        // batch_max)
+        const int want = src ? max(kShareBatch, min(kc_batch_max, ((pool - we) >> 3) & ~63)) : 64;
+        const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
+        if (lane == leader) {
+          if (src) {
+            const unsigned long long wd = __hip_atomic_fetch_add(src, static_cast<unsigned long long>(want),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g = static_cast<int>(static_cast<unsigned>(wd));
+            if (g < pool) atomicAdd(&s_cnt, min(pool - g, want));
+            atomicMax(&s_join, word_helpers(wd));
+          } else {
+            g = atomicAdd(&s_pool_next, 64);
+          }
+        }
+        g = __builtin_amdgcn_readlane(g, leader);
+        wb = min(g, pool);
+        we = min(g + want, pool);
+        if (wb >= pool) we = pool;   // spent: the lanes left over retire
+      }
+      if (done) {
+        j = nj;
+        fresh = true;
+        if (nj < 0) active = false;
+      }
     }
     if constexpr (STATS) st_c_acc += stamp() - st_ts;
   }
@@ -1151,26 +1359,57 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // thread t < 3 * npx writes channel t % 3 of pool pixel t / 3: a tile row's
   // 8 pixels are 24 consecutive floats
   __syncthreads();
+  const KArgsP ke = kargs_opaque();
   const int t = static_cast<int>(threadIdx.x);
-  if (t < npx * 3) {
-    const int fp = t / 3, ch = t - 3 * fp;
+  // (owner of an unshared tile: no helper joined before its pool was spent)
+  const bool alone = !shared_tile || sgpr(s_join) == 0;
+  auto out_index = [&](int tt) {
+    const int fp = tt / 3, ch = tt - 3 * fp;
     const int qy = vw == 1 ? fp : static_cast<int>(__umulhi(static_cast<uint32_t>(fp), mag_vw));
     const int px = qx0 + (fp - qy * vw), ro = qy0 + qy;
-    const size_t e = (static_cast<size_t>(ro) * a.width + px) * 3 + ch;
-    if (split) {   // one split's integer sum; finalize_kernel adds the splits (order-free)
-      a.part[static_cast<size_t>(split_ix) * a.rows_out * a.width * 3 + e] = s_acc[t];
-    } else {
-      const float tot = static_cast<float>(s_acc[t]) * 0x1p-24f;   // RN(float(sum)), exact scale
-      const float inv = static_cast<float>(a.spp > 0 ? a.spp : 1);
-      // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
-      a.out[e] = a.realm ? tot * (1.0f / inv) : tot / inv;
+    return (static_cast<size_t>(ro) * ke->width + px) * 3 + ch;
+  };
+  auto write_mean = [&](size_t e, unsigned long long sum) {
+    const float tot = static_cast<float>(sum) * 0x1p-24f;   // RN(float(sum)), exact scale
+    const float inv = static_cast<float>(ke->spp > 0 ? ke->spp : 1);
+    // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
+    ke->out[e] = ke->realm ? tot * (1.0f / inv) : tot / inv;
+  };
+  if (split) {   // one split's integer sum; finalize_kernel adds the splits (order-free)
+    if (t < npx * 3) ke->part[static_cast<size_t>(split_ix) * ke->rows_out * ke->width * 3 + out_index(t)] = s_acc[t];
+  } else if (alone) {   // every sample of the tile was this workgroup's
+    if (t < npx * 3) write_mean(out_index(t), s_acc[t]);
+  } else {
+    // a shared tile (owner or helper): the integer sums
+    // meet in sum[tile] (atomics: any order, the same total); the workgroup
+    // whose samples complete the pool converts them and re-zeroes the slots
+    unsigned long long* gs = ke->sum + static_cast<size_t>(tile) * (NPX * 3);
+    if (t < npx * 3 && s_acc[t])
+      __hip_atomic_fetch_add(&gs[t], s_acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned mine = static_cast<unsigned>(s_cnt);
+      const unsigned prev = __hip_atomic_fetch_add(&ke->done[tile], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = prev + mine == static_cast<unsigned>(pool);
+    }
+    __syncthreads();
+    if (sgpr(s_last)) {   // (every participant has added: the slots and done are free for the next use)
+      if (t < npx * 3)
+        write_mean(out_index(t), __hip_atomic_exchange(&gs[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (t == 0) __hip_atomic_exchange(&ke->done[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
-  if (a.tile_cost && threadIdx.x == 0) {   // the adaptive schedule's measurement: the workgroup's time
+  if (ke->tile_cost && threadIdx.x == 0) {   // the adaptive schedule's measurement: the unit's time
     const uint64_t dt = __builtin_amdgcn_s_memrealtime() - st_t0;
-    atomicAdd(&a.tile_cost[tile], static_cast<unsigned>(dt < 0xffffffffull ? dt : 0xffffffffull));
+    atomicAdd(&ke->tile_cost[tile], static_cast<unsigned>(dt < 0xffffffffull ? dt : 0xffffffffull));
   }
+  if (ke->counters && own && threadIdx.x == 0 && pool)
+    atomicAdd(&ke->counters[1], static_cast<unsigned long long>(pool));
+
   if constexpr (STATS) {
     if (a.dbg && st_iter) {
       atomicAdd(&a.dbg[0], static_cast<unsigned long long>(st_iter));
@@ -1226,7 +1465,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
   // wave timeline (stats variants, or any variant under RTCLJ_TIMELINE in
   // the diagnostic build; NULL otherwise: a uniform branch)
   if (a.dbgw && lane == 0) {
-    const size_t wid = static_cast<size_t>(slot) * 4 + (threadIdx.x >> 6);   // by dispatch slot
+    const size_t wid = static_cast<size_t>(unit) * 4 + (threadIdx.x >> 6);   // by dispatch slot
     if (wid < 65536) {
       a.dbgw[4 * wid + 0] = st_t0;
       a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1240,7 +1479,6 @@ __global__ __launch_bounds__(256) void trace_kernel(const KArgs a) {
     uint32_t v = segs;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0 && v) atomicAdd(&a.counters[0], static_cast<unsigned long long>(v));
-    if (threadIdx.x == 0 && pool) atomicAdd(&a.counters[1], static_cast<unsigned long long>(pool));
   }
 }
 
@@ -1435,6 +1673,15 @@ struct Schedule {
   ScheduleKey key{};
   unsigned long long* part = nullptr;   // [split][rows][width][3] pixel sums of split tiles
   size_t part_cap = 0;                  // u64 elements
+  // the stealing state (KArgs word, done, sum, owner, stealc)
+  unsigned long long* word = nullptr;   // per tile
+  unsigned* done = nullptr;             // per tile
+  unsigned long long* sum = nullptr;    // per tile x kPoolPx x 3, zero between uses
+  int steal_cap = 0;                    // tiles those hold
+  int* owner = nullptr;                 // KArgs n_owner entries
+  int owner_cap = 0;
+  unsigned long long* stealc = nullptr; // [helpers that got samples, their first samples] since rt_steal_stats
+  unsigned epoch = 0;                   // launches with sharing on this stream
 };
 constexpr int kSchedStreams = 8;
 struct ScheduleSet {
@@ -1445,6 +1692,11 @@ struct ScheduleSet {
     if (e.cost) (void)hipFree(e.cost);
     if (e.order) (void)hipFree(e.order);
     if (e.part) (void)hipFree(e.part);
+    if (e.word) (void)hipFree(e.word);
+    if (e.done) (void)hipFree(e.done);
+    if (e.sum) (void)hipFree(e.sum);
+    if (e.owner) (void)hipFree(e.owner);
+    if (e.stealc) (void)hipFree(e.stealc);
     e = Schedule{};
   }
   void release() {
@@ -1753,6 +2005,15 @@ static const int kSplitRounds = [] {
 }();
 constexpr int kSplitMax = 64;
 
+// Tile sharing, A/B knobs read at every launch:
+// RTCLJ_STEAL=0 (off: the static sample split for launches of few tiles, as
+// before), RTCLJ_THIEVES (helper workgroups per workgroup slot of the
+// device), RTCLJ_STEAL_MIN (unclaimed samples a tile needs for a helper to join)
+static int env_int(const char* name, int dflt, int lo) {
+  const char* e = std::getenv(name);
+  return e ? std::max(lo, std::atoi(e)) : dflt;
+}
+
 // workgroups device `device` holds at once for kernel fn with `lds` bytes of
 // dynamic LDS (CUs x the occupancy query), cached per (device, fn, lds)
 static int launch_slots(int device, const void* fn, size_t lds) {
@@ -1866,7 +2127,14 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // The integer pixel sums add up to the same bits in any grouping.
   // (The kernel also takes a whole-tile prefix of the order, n_whole; the
   // split tiles' partial sums go through finalize_kernel.)
+  // (Tile sharing, below, takes the launches that are not split: a split
+  // launch has about one unit per workgroup slot, all of which end together,
+  // and on C1's 8-GPU shard the split is faster -- 1.05 vs 1.09-1.18 ms --
+  // while sharing balances the tail of a long launch in plain order, C1
+  // 6.78 -> 6.47 ms, and in the record's longest-first order costs nothing
+  // (profiles/r03/share_ab.txt).  RTCLJ_STEAL=0: never share.)
   int split = 1, n_whole = n_tiles;
+  const bool steal = sch && env_int("RTCLJ_STEAL", 1, 0) != 0 && !v.stats;
   if (sch && p->spp > 1) {
     if (const char* e = std::getenv("RTCLJ_SPLIT")) {
       split = std::max(1, std::atoi(e));
@@ -1909,7 +2177,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // adaptive schedule: dispatch tiles longest first, by the durations the
   // previous launches of this launch shape on this scene and stream measured
   // (each launch's added to half the record before it)
-  if (sch && g_schedule.load() == 0) {
+  bool new_shape = false;
+  if (sch) {
     ScheduleKey key{};
     key.width = a.width;
     key.rows = a.rows_out;
@@ -1922,7 +2191,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     if (std::memcmp(&sch->key, &key, sizeof key) != 0) {
       sch->ready = false;
       sch->key = key;
+      new_shape = true;
     }
+  }
+  if (sch && g_schedule.load() == 0) {
     if (sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
       HIP_TRY(hipStreamSynchronize(stream));
       if (sch->cost) (void)hipFree(sch->cost);
@@ -1941,8 +2213,73 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // when this launch shape starts a new history
     if (!sch->ready) HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
   }
+  // the grid: the units, then (stealing) the thieves, dispatched last, i.e.
+  // as the units' slots free up in the launch's tail
+  int64_t grid = n_units;
+  if (steal && split == 1) {
+    const int slots = std::max(1, launch_slots(ds->device, v.fn, lds));
+    const int n_owner = 2 * slots;   // owner entries: twice the resident workgroups
+    // (at most 32 per slot: a tile's helper count stays below 2^16)
+    grid += static_cast<int64_t>(std::min(32, env_int("RTCLJ_THIEVES", 4, 0))) * slots;
+    if (grid > INT_MAX) grid = n_units;
+    if (!sch->stealc) {
+      HIP_TRY(hipMalloc(&sch->stealc, 2 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemsetAsync(sch->stealc, 0, 2 * sizeof(unsigned long long), stream));
+    }
+    if (sch->steal_cap < n_tiles) {   // grow: this stream's kernels may still use the old buffers
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->word) (void)hipFree(sch->word);
+      if (sch->done) (void)hipFree(sch->done);
+      if (sch->sum) (void)hipFree(sch->sum);
+      sch->word = nullptr;
+      sch->done = nullptr;
+      sch->sum = nullptr;
+      sch->steal_cap = 0;
+      const size_t nsum = static_cast<size_t>(n_tiles) * kPoolPx * 3;
+      HIP_TRY(hipMalloc(&sch->word, n_tiles * sizeof(unsigned long long)));
+      HIP_TRY(hipMalloc(&sch->done, n_tiles * sizeof(unsigned)));
+      HIP_TRY(hipMalloc(&sch->sum, nsum * sizeof(unsigned long long)));
+      // words 0: lo = hi, nothing to steal until an owner publishes; sums
+      // and done counts 0 (the kernel keeps them so between uses)
+      HIP_TRY(hipMemsetAsync(sch->word, 0, n_tiles * sizeof(unsigned long long), stream));
+      HIP_TRY(hipMemsetAsync(sch->done, 0, n_tiles * sizeof(unsigned), stream));
+      HIP_TRY(hipMemsetAsync(sch->sum, 0, nsum * sizeof(unsigned long long), stream));
+      sch->steal_cap = n_tiles;
+      new_shape = true;
+    }
+    if (sch->owner_cap != n_owner) {
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->owner) (void)hipFree(sch->owner);
+      sch->owner = nullptr;
+      sch->owner_cap = 0;
+      HIP_TRY(hipMalloc(&sch->owner, n_owner * sizeof(int)));
+      sch->owner_cap = n_owner;
+      new_shape = true;
+    }
+    sch->epoch = (sch->epoch + 1) & 0xffffu;
+    if (sch->epoch == 0) {   // wrapped: no owner entry may name a word of the epoch's last use
+      sch->epoch = 1;
+      new_shape = true;
+    }
+    a.epoch = sch->epoch;
+    // a new shape: no tile is being run (old entries would only name words
+    // of other epochs, but tile indices of another shape may exceed this one's)
+    if (new_shape) HIP_TRY(hipMemsetAsync(sch->owner, 0xff, n_owner * sizeof(int), stream));
+    a.word = sch->word;
+    a.done = sch->done;
+    a.sum = sch->sum;
+    a.owner = sch->owner;
+    a.n_owner = n_owner;
+    a.stealc = sch->stealc;
+    a.steal_min = env_int("RTCLJ_STEAL_MIN", 256, 1);
+    // claims of up to 1024 samples in the record's longest-first order (the
+    // heavy tiles start first: fewer claims, 6.03 -> 6.00 ms on C1), of 128
+    // in plain order (helpers then need small claims to balance the tail)
+    a.batch_max = env_int("RTCLJ_BATCH_MAX", a.tile_order ? 1024 : kShareBatch, kShareBatch);
+  }
+  a.n_units = n_units;
   void* args[] = {&a};
-  HIP_TRY(hipLaunchKernel(v.fn, dim3(n_units), block, args, lds, stream));
+  HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
   if (split > 1) {
     const unsigned long long* part = a.part;
     const int* order = a.tile_order;
@@ -1980,6 +2317,25 @@ extern "C" int rt_debug_stats(uint64_t* out32) {
     HIP_TRY(hipMemcpy(v, g_dbg[d], sizeof v, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(g_dbg[d], 0, sizeof v));
     for (int i = 0; i < kDbg; ++i) out32[i] += v[i];
+  }
+  return RT_OK;
+}
+
+// Steals of the launches on (ds, stream) since the last call: out2 =
+// {steals, samples stolen}; waits for the stream, then clears them.
+extern "C" int rt_steal_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2) {
+  clear_error();
+  if (!ds || !out2) return set_error(RT_E_ARG, "rt_steal_stats: NULL argument");
+  out2[0] = out2[1] = 0;
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  std::lock_guard<std::mutex> lk(ds->sched.mu);
+  for (int k = 0; k < ds->sched.used; ++k) {
+    const Schedule& e = ds->sched.s[k];
+    if (e.stream != stream || !e.stealc) continue;
+    HIP_TRY(hipSetDevice(ds->device));
+    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(hipMemcpy(out2, e.stealc, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(e.stealc, 0, 2 * sizeof(uint64_t)));
   }
   return RT_OK;
 }
