@@ -85,9 +85,12 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant; 0 = default)")
     ap.add_argument("--schedule", type=int, default=0,
                     help="tile schedule (rt_set_schedule): 0 adaptive longest-first, 1 plain dispatch order")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames go round-robin to this many streams "
-                         "(rt_launch RT_FLAG_STREAMED when > 1); 1 = one stream, one frame at a time")
+                         "(rt_launch RT_FLAG_STREAMED when > 1); 1 = one stream, one frame at a time. "
+                         "Default: 1 on one GPU (each timed frame is one kernel, so the rocprof kernel "
+                         "durations are the frame times; a second stream gains ~1 %% there), 2 on several "
+                         "(a shard's frame is ~1 ms: the next frame fills its tail, DESIGN.md §6)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -99,6 +102,8 @@ def parse():
         a.steps = 100 if a.workload == "c1" else 5
     if a.warmup is None:
         a.warmup = 5 if a.workload == "c1" else 1
+    if a.inflight is None:
+        a.inflight = 1 if a.gpus == 1 else 2
     return a
 
 

@@ -145,21 +145,26 @@ typedef struct rt_stats {
   double total_ms;        /* wall time of the whole call incl. H2D/D2H         */
   int n_devices;          /* devices used                                      */
   int scene_cached;       /* devices whose scene came from the library's cache */
-  double upload_ms;       /* max over devices: scene lookup / H2D upload + BVH  */
-  double gather_ms;       /* max over devices: D2H into pinned memory + host
-                             scatter of the device's row tiles into out_rgb    */
+  double upload_ms;       /* max over devices: the wait for the scene's upload +
+                             BVH builds (a cache miss; they run beside the
+                             render-context set-up, this is what is left)      */
+  double gather_ms;       /* max over devices: D2H of the device's row tiles
+                             into their rows of out_rgb (strided copies)       */
   double kernel_ms_mean;  /* mean over devices of the trace-kernel time
                              (load imbalance = kernel_ms / kernel_ms_mean)     */
   /* Where the wall time of the slowest device's share went (host clocks, in
-   * order): upload_ms above, then these; the rest of total_ms (argument
-   * checks, thread fan-out and join) is other_ms.  A first call shows its
-   * one-time costs here: setup_ms (the device's stream, events, device
-   * framebuffer, pinned buffers) and enqueue_ms (the first launch loads the
-   * kernels' code object).                                                   */
+   * order): setup_ms, upload_ms above, then the others; the rest of total_ms
+   * (argument checks, thread fan-out and join) is other_ms.  A first call
+   * shows its one-time costs here: setup_ms (events, device framebuffer,
+   * pinned counters; a device's first context runs on its NULL stream, a
+   * created stream costs 5-7 ms), upload_ms (what the scene upload and BVH
+   * builds add beyond the set-up they run beside) and enqueue_ms (the first
+   * launch loads the kernels' code object).                                  */
   double setup_ms;        /* render context set-up                             */
   double enqueue_ms;      /* rt_launch + D2H enqueue                           */
   double wait_ms;         /* host wait for the device: kernel + D2H            */
-  double scatter_ms;      /* host scatter of row tiles (several devices)       */
+  double scatter_ms;      /* host scatter of row tiles: 0 since ABI 3's
+                             strided copies place the rows                    */
   double other_ms;        /* total_ms - upload - setup - enqueue - wait - scatter */
   double d2h_ms;          /* max over devices: event-timed D2H of the frame    */
 } rt_stats;
@@ -226,8 +231,9 @@ int rt_scene_cover(int grid, uint64_t seed, float* sphere, int* kind, float* mat
 int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p,
               float* out_rgb, size_t out_len, rt_stats* stats);
 
-/* Drop rt_render's cached device scenes, streams and staging buffers (those
- * not in use by a concurrent call).  Returns the number of scenes dropped. */
+/* Drop rt_render's cached device scenes and render contexts (streams,
+ * buffers; those not in use by a concurrent call).  Returns the number of
+ * scenes dropped. */
 int rt_cache_clear(void);
 
 /* Device-resident path (inputs already in HBM; used by the benchmark). */

@@ -9,7 +9,7 @@
 //                here: N devices, interleaved 8-row tiles for balance)
 //
 // rt_render keeps, per device, the uploaded scenes (by content) and a few
-// render contexts (stream, device framebuffer, pinned staging buffer), so a
+// render contexts (stream, device framebuffer, pinned counters), so a
 // repeated call pays neither the upload and BVH builds nor the allocations,
 // and its launches reuse the stream whose adaptive tile order the previous
 // call recorded.
@@ -202,17 +202,18 @@ bool same_scene(const CachedScene& c, const rt_scene& s) {
 // ---- per-device render context: stream, buffers, events ---------------------
 struct Ctx {
   int device = 0;
+  // the device's NULL stream (its first context: creating a stream takes
+  // 5-7 ms on MI355X, tools/first_call.cpp -- most of a first call's set-up)
+  bool null_stream = false;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
   float* d_out = nullptr;
   size_t d_cap = 0;           // floats
-  float* h_pin = nullptr;     // pinned staging for the D2H
-  size_t h_cap = 0;           // floats
   uint64_t* d_cnt = nullptr;
   uint64_t* h_cnt = nullptr;  // pinned
   ~Ctx() {
     (void)hipSetDevice(device);
-    if (stream) {
+    if (stream || null_stream) {
       (void)hipStreamSynchronize(stream);
       release_stream_schedules(device, stream);   // the scenes' per-stream slots
     }
@@ -221,7 +222,6 @@ struct Ctx {
     if (e2) (void)hipEventDestroy(e2);
     if (d_out) (void)hipFree(d_out);
     if (d_cnt) (void)hipFree(d_cnt);
-    if (h_pin) (void)hipHostFree(h_pin);
     if (h_cnt) (void)hipHostFree(h_cnt);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -238,11 +238,29 @@ struct DeviceCache {
   std::mutex upload_mu;   // one upload at a time: concurrent misses of one scene build it once
   std::vector<CachedScene> scenes;
   std::vector<std::unique_ptr<Ctx>> free_ctx;
+  // the context on the device's NULL stream, while idle (primary_made: it
+  // exists, idle or in use)
+  std::unique_ptr<Ctx> primary;
+  bool primary_made = false;
   uint64_t tick = 0;
 };
 // never destroyed: HIP may already be torn down when static destructors run
 std::vector<DeviceCache>* g_cache = new std::vector<DeviceCache>(64);
 std::mutex g_cache_mu;
+
+// the cached device scene of s on `device`, if there is one
+bool find_scene(int device, const rt_scene* s, std::shared_ptr<rt_dscene>* out) {
+  DeviceCache& dc = (*g_cache)[device];
+  const uint64_t h = scene_hash(*s);
+  std::lock_guard<std::mutex> lk(dc.mu);
+  for (CachedScene& c : dc.scenes)
+    if (c.hash == h && same_scene(c, *s)) {
+      c.last_use = ++dc.tick;
+      *out = c.ds;
+      return true;
+    }
+  return false;
+}
 
 // the cached device scene of s on `device`, uploading it on a miss.  Shards
 // of one call that share a device (RT_FLAG_SHARDS_ON_DEVICE0) and concurrent
@@ -294,6 +312,14 @@ std::unique_ptr<Ctx> take_ctx(int device) {
   DeviceCache& dc = (*g_cache)[device];
   {
     std::lock_guard<std::mutex> lk(dc.mu);
+    if (!dc.primary_made) {   // the first context of the device: its NULL stream
+      dc.primary_made = true;
+      auto c = std::make_unique<Ctx>();
+      c->device = device;
+      c->null_stream = true;
+      return c;
+    }
+    if (dc.primary) return std::move(dc.primary);
     if (!dc.free_ctx.empty()) {
       std::unique_ptr<Ctx> c = std::move(dc.free_ctx.back());
       dc.free_ctx.pop_back();
@@ -307,7 +333,8 @@ std::unique_ptr<Ctx> take_ctx(int device) {
 void give_ctx(std::unique_ptr<Ctx> c) {
   DeviceCache& dc = (*g_cache)[c->device];
   std::lock_guard<std::mutex> lk(dc.mu);
-  if (static_cast<int>(dc.free_ctx.size()) < kFreeCtx) dc.free_ctx.push_back(std::move(c));
+  if (c->null_stream) dc.primary = std::move(c);
+  else if (static_cast<int>(dc.free_ctx.size()) < kFreeCtx) dc.free_ctx.push_back(std::move(c));
 }
 
 struct Shard {
@@ -320,13 +347,13 @@ struct Shard {
   float ms = 0.0f, d2h_ms = 0.0f;
   // host clocks of the share, in order (rt_stats)
   double upload_ms = 0.0, setup_ms = 0.0, enqueue_ms = 0.0, wait_ms = 0.0, scatter_ms = 0.0, wall_ms = 0.0;
-  double gather_ms = 0.0;   // d2h_ms + scatter_ms
+  double gather_ms = 0.0;   // d2h_ms (+ scatter_ms, 0: no host scatter)
   bool cached = false;
 };
 
-// one device's share: scene (cached), launch, D2H into pinned staging, then
-// the host scatter of its compacted row tiles into out_rgb (disjoint rows:
-// the shards scatter in parallel, each as soon as its own device is done)
+// one device's share: scene (cached), launch, D2H of its compacted row
+// tiles straight into their rows of out_rgb (disjoint rows: the shards copy
+// in parallel, each as soon as its own device is done)
 void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb, int rows_total, int ntiles,
                int nshards, int shard_idx) {
   auto fail = [&](int code) {
@@ -339,14 +366,25 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
   };
   const auto t0 = Clock::now();
   std::shared_ptr<rt_dscene> ds;
-  int rc = get_scene(sh->device, s, &ds, &sh->cached);
-  if (rc != RT_OK) return fail(rc);
-  sh->upload_ms = ms_since(t0);
+  int rc = RT_OK;
+  // the scene: from the cache, or (a miss: upload and BVH builds, ~1-3 ms)
+  // on a helper thread while this one sets up the render context, the other
+  // one-time cost of a first call (stream, events, buffers)
+  std::thread upload;
+  std::string upload_err;   // (the error slot is per thread)
+  if (!find_scene(sh->device, s, &ds)) {
+    upload = std::thread([&] {
+      rc = get_scene(sh->device, s, &ds, &sh->cached);
+      if (rc != RT_OK) upload_err = rt_last_error();
+    });
+  } else {
+    sh->cached = true;
+  }
   const auto t_setup = Clock::now();
   std::unique_ptr<Ctx> cx = take_ctx(sh->device);
   const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
   hipError_t e = hipSetDevice(sh->device);
-  if (e == hipSuccess && !cx->stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess && !cx->stream && !cx->null_stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && !cx->e0) e = hipEventCreate(&cx->e0);
   if (e == hipSuccess && !cx->e1) e = hipEventCreate(&cx->e1);
   if (e == hipSuccess && !cx->e2) e = hipEventCreate(&cx->e2);
@@ -359,14 +397,17 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
     e = hipMalloc(&cx->d_out, std::max<size_t>(nfl, 1) * sizeof(float));
     if (e == hipSuccess) cx->d_cap = nfl;
   }
-  if (e == hipSuccess && nshards > 1 && cx->h_cap < nfl) {   // staging: only several shards scatter from it
-    if (cx->h_pin) (void)hipHostFree(cx->h_pin);
-    cx->h_pin = nullptr;
-    cx->h_cap = 0;
-    e = hipHostMalloc(&cx->h_pin, std::max<size_t>(nfl, 1) * sizeof(float), hipHostMallocDefault);
-    if (e == hipSuccess) cx->h_cap = nfl;
-  }
   sh->setup_ms = ms_since(t_setup);
+  // upload_ms: the part of the upload the call waited for after its set-up
+  const auto t_up = Clock::now();
+  if (upload.joinable()) upload.join();
+  sh->upload_ms = ms_since(t_up);
+  if (rc != RT_OK) {
+    if (e == hipSuccess) give_ctx(std::move(cx));
+    sh->status = rc;
+    sh->err = upload_err;
+    return;
+  }
   const auto t_enq = Clock::now();
   if (e == hipSuccess) e = hipMemsetAsync(cx->d_cnt, 0, 2 * sizeof(uint64_t), cx->stream);
   if (e == hipSuccess) e = hipEventRecord(cx->e0, cx->stream);
@@ -378,13 +419,32 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
       fail(rc);
     } else {
       e = hipEventRecord(cx->e1, cx->stream);
-      // one shard: straight into the caller's buffer (measured on MI355X for
-      // a C1 frame: 0.46-0.52 ms, against 0.53-0.56 ms into pinned staging
-      // plus 0.34 ms of host copy, tools/d2h_bench.cpp); several: into the
-      // pinned staging, then each shard scatters its row tiles
-      if (e == hipSuccess && nfl)
-        e = hipMemcpyAsync(nshards == 1 ? out_rgb : cx->h_pin, cx->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost,
-                           cx->stream);
+      // straight into the caller's buffer (measured on MI355X for a C1
+      // frame: 0.46-0.52 ms, against 0.53-0.56 ms into pinned staging plus
+      // 0.34 ms of host copy, tools/d2h_bench.cpp).  Several shards: the
+      // shard's compacted row tiles land in their image rows through one
+      // strided copy (tile k of the shard -> image tile shard_idx + k *
+      // nshards), the image's last tile, if it is short, through a second
+      if (e == hipSuccess && nfl) {
+        if (nshards == 1) {
+          e = hipMemcpyAsync(out_rgb, cx->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, cx->stream);
+        } else {
+          const int T = sh->p.row_tile;
+          const size_t rowb = static_cast<size_t>(sh->p.width) * 3 * sizeof(float);
+          const int ntile = (ntiles - shard_idx + nshards - 1) / nshards;   // this shard's tiles
+          const int t_last = shard_idx + (ntile - 1) * nshards;
+          const bool short_last = t_last == ntiles - 1 && rows_total % T != 0;
+          const int nfull = ntile - (short_last ? 1 : 0);
+          if (nfull > 0)
+            e = hipMemcpy2DAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(shard_idx) * T * rowb,
+                                 static_cast<size_t>(nshards) * T * rowb, cx->d_out, T * rowb, T * rowb, nfull,
+                                 hipMemcpyDeviceToHost, cx->stream);
+          if (e == hipSuccess && short_last)
+            e = hipMemcpyAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(t_last) * T * rowb,
+                               reinterpret_cast<const char*>(cx->d_out) + static_cast<size_t>(nfull) * T * rowb,
+                               static_cast<size_t>(rows_total - t_last * T) * rowb, hipMemcpyDeviceToHost, cx->stream);
+        }
+      }
       if (e == hipSuccess)
         e = hipMemcpyAsync(cx->h_cnt, cx->d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, cx->stream);
       if (e == hipSuccess) e = hipEventRecord(cx->e2, cx->stream);
@@ -401,21 +461,8 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
       } else {
         sh->counters[0] = cx->h_cnt[0];
         sh->counters[1] = cx->h_cnt[1];
-        // host scatter: compacted tiles back to their image rows
-        const auto ts = Clock::now();
-        const size_t rowf = static_cast<size_t>(sh->p.width) * 3;
-        if (nshards > 1) {
-          const int T = sh->p.row_tile;
-          int ro = 0;
-          for (int t = shard_idx; t < ntiles; t += nshards) {
-            const int r0 = t * T, nr = std::min(T, rows_total - r0);
-            std::memcpy(out_rgb + static_cast<size_t>(r0) * rowf, cx->h_pin + static_cast<size_t>(ro) * rowf,
-                        nr * rowf * sizeof(float));
-            ro += nr;
-          }
-        }
-        sh->scatter_ms = ms_since(ts);
-        sh->gather_ms = d2h + sh->scatter_ms;
+        sh->scatter_ms = 0.0;   // (no host scatter: the copies place the rows)
+        sh->gather_ms = d2h;
       }
     }
   }
@@ -435,6 +482,10 @@ extern "C" int rt_cache_clear(void) {
       std::lock_guard<std::mutex> l2(dc.mu);
       scenes.swap(dc.scenes);
       ctxs.swap(dc.free_ctx);
+      if (dc.primary) {   // (one in use stays; it is dropped at a later clear)
+        ctxs.push_back(std::move(dc.primary));
+        dc.primary_made = false;
+      }
     }
     dropped += static_cast<int>(scenes.size());
   }
