@@ -59,7 +59,8 @@ METRIC = "Mray-samples/sec at 1200×675×100spp depth50; achieved HBM GB/s vs pe
 def metric_for(width, height, spp, depth):
     return f"Mray-samples/sec at {width}×{height}×{spp}spp depth{depth}; achieved HBM GB/s vs peak"
 
-PMC_DIR = ROOT / "profiles" / "r02" / "pmc_c1"
+# committed rocprofv3 PMC passes of the current build (profiles/pmc.sh), per workload
+PMC_DIRS = {"c1": ROOT / "profiles" / "r03" / "pmc_c1", "c4": ROOT / "profiles" / "r03" / "pmc_c4"}
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -244,13 +245,13 @@ def lib_resolved_variant(scene, device):
     return _resolved[(id(scene), device)]
 
 
-def _pmc_avg(passes, counters):
+def _pmc_avg(pmc_dir, passes, counters):
     """Per-dispatch averages of PMC counters over the product kernel's
     launches (trace_kernel, not the stats build) in the committed rocprofv3
     passes (profiles/pmc.sh; one counter group per pass)."""
     acc = {}
     for name in passes:
-        f = PMC_DIR / f"{name}.csv"
+        f = pmc_dir / f"{name}.csv"
         if not f.exists():
             return None
         for r in csv.DictReader(open(f)):
@@ -261,23 +262,23 @@ def _pmc_avg(passes, counters):
     return {c: sum(v) / len(v) for c, v in acc.items()}
 
 
-def pmc_traffic():
+def pmc_traffic(pmc_dir):
     """HBM bytes per launch (FETCH_SIZE and WRITE_SIZE in their own passes, KB
     units; gfx950's FETCH_SIZE counts half the bytes of wide streaming reads ->
     x2, MI355X_MICROARCH.md §HBM)."""
-    v = _pmc_avg(("fetch", "write"), ("FETCH_SIZE", "WRITE_SIZE"))
+    v = _pmc_avg(pmc_dir, ("fetch", "write"), ("FETCH_SIZE", "WRITE_SIZE"))
     if v is None:
         return None
     return {"bytes": (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0, "fetch_bytes_x2": 2048.0 * v["FETCH_SIZE"],
-            "write_bytes": 1024.0 * v["WRITE_SIZE"], "source": str(PMC_DIR.relative_to(ROOT))}
+            "write_bytes": 1024.0 * v["WRITE_SIZE"], "source": str(pmc_dir.relative_to(ROOT))}
 
 
-def pmc_valu(n_simd=1024, n_xcd=8):
+def pmc_valu(pmc_dir, n_simd=1024, n_xcd=8):
     """VALU issue picture of the same launches: issue_busy = fraction of
     4-cycle slots in which a SIMD issues a VALU instruction
     (SQ_ACTIVE_INST_VALU x 4 / SIMDs vs GRBM_GUI_ACTIVE / XCDs); lanes_active
     = mean fraction of the 64 lanes active per VALU instruction."""
-    v = _pmc_avg(("insts", "waves"), ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU",
+    v = _pmc_avg(pmc_dir, ("insts", "waves"), ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU",
                                       "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES"))
     if v is None:
         return None
@@ -286,7 +287,7 @@ def pmc_valu(n_simd=1024, n_xcd=8):
     return {"issue_busy": busy, "lanes_active": lanes, "issue_utilisation": busy * lanes,
             "valu_insts": v["SQ_INSTS_VALU"],
             "mean_waves_per_simd": v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd),
-            "source": str(PMC_DIR.relative_to(ROOT))}
+            "source": str(pmc_dir.relative_to(ROOT))}
 
 
 def occupancy(ds, p):
@@ -523,9 +524,9 @@ def main():
         launch_samples = rows * W * spp
         launch_segs = seg_per_sample * launch_samples
         kms = [r["kernel_ms_avg"] for r in per_rank]
-        pmc_ok = a.workload == "c1" and not a.spp and a.variant == 0 and world == 1
-        traffic = pmc_traffic() if pmc_ok else None
-        valu = pmc_valu() if pmc_ok else None
+        pmc_dir = PMC_DIRS.get(a.workload) if (not a.spp and a.variant == 0 and world == 1) else None
+        traffic = pmc_traffic(pmc_dir) if pmc_dir else None
+        valu = pmc_valu(pmc_dir) if pmc_dir else None
         bf_flops = launch_segs * (FLOPS_PER_SPHERE * len(scene) + FLOPS_PER_SEGMENT_NOMINAL)
         bf_tflops = bf_flops / (kern_avg_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
@@ -567,7 +568,11 @@ def main():
                              "frac": gbs / PEAK_HBM_GBS, "traffic": traffic["bytes"] if traffic else None,
                              "traffic_detail": traffic,
                              "note": "non-binding: algorithmic bytes/launch = W*rows*12 (fp32 RGB written once) + "
-                                     "bodies*32 (scene read); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch"},
+                                     "bodies*32 (scene read); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch. "
+                                     "Beyond the algorithmic bytes: the 12-byte pixels' partial 64-B lines, and the tile "
+                                     "sharing's global atomics (each wave's batch claims on its tile's word, the helper "
+                                     "workgroups' owner-table reads and shared tiles' sums; DESIGN.md §3.1), not "
+                                     "re-reads"},
             "valu": valu, "occupancy": occ, "stats_build": stats,
             "kernel_ms_avg": kern_avg_ms, "launch_span_ms_max": mine["kernel_ms_max"],
             "dispatch_order": {"kernel_ms": mine["first_launch_ms"],
