@@ -35,6 +35,7 @@ import ctypes as C
 import json
 import os
 import platform
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -259,7 +260,10 @@ def _pmc_avg(pmc_dir, passes, counters):
                 acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     if any(c not in acc for c in counters):
         return None
-    return {c: sum(v) / len(v) for c, v in acc.items()}
+    # the median launch: the timed frames' recorded order, not the run's
+    # first launch or the plain-order one (tile sharing claims in small
+    # batches there)
+    return {c: statistics.median(v) for c, v in acc.items()}
 
 
 def pmc_traffic(pmc_dir):

@@ -119,7 +119,7 @@ struct alignas(16) KArgs {
   int n_owner;
   int n_units;
   int steal_min;
-  int batch_max;                 // a wave's largest claim on a shared tile
+  int batch_max;                 // a wave's largest claim on a shared tile (0: by the pool)
   unsigned epoch;                // this launch's (per stream, 1 .. 65535)
 };
 
@@ -492,7 +492,8 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // where the waves claim their batches: the shared tile's word, else (NULL)
   // the workgroup's s_pool_next
   unsigned long long* const src = shared_tile ? ka->word + tile : nullptr;
-  const int kc_batch_max = ka->batch_max;
+  // (batch_max 0: by the pool, 1/48 of it, 128 .. 1024)
+  const int kc_batch_max = ka->batch_max > 0 ? ka->batch_max : min(1024, max(kShareBatch, (pool / 48) & ~63));
   if (threadIdx.x == 0) {
     if (own && shared_tile) {
       __hip_atomic_exchange(&ka->word[tile], (static_cast<unsigned long long>(ka->epoch) << 48) | 256ull,
@@ -2282,9 +2283,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     a.stealc = sch->stealc;
     a.steal_min = env_int("RTCLJ_STEAL_MIN", 256, 1);
     // claims of up to 1024 samples in the record's longest-first order (the
-    // heavy tiles start first: fewer claims, 6.03 -> 6.00 ms on C1), of 128
-    // in plain order (helpers then need small claims to balance the tail)
-    a.batch_max = env_int("RTCLJ_BATCH_MAX", a.tile_order ? 1024 : kShareBatch, kShareBatch);
+    // heavy tiles start first: fewer claims, 6.03 -> 6.00 ms on C1); in plain
+    // order up to 1/48 of the tile's pool (0: the kernel's per-pool rule; C1's
+    // 6,400: 128 -- helpers then need small claims to balance the tail;
+    // C4's 64,000: 1024)
+    a.batch_max = env_int("RTCLJ_BATCH_MAX", a.tile_order ? 1024 : 0, 0);
   }
   a.n_units = n_units;
   void* args[] = {&a};

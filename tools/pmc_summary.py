@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Summarise committed rocprofv3 PMC passes (profiles/pmc.sh) of the product
-kernel: per-dispatch averages of every counter over trace_kernel<..., false>
+kernel: per-dispatch medians of every counter over trace_kernel<..., false>
 launches, plus the derived VALU / occupancy / HBM figures bench.py reports.
 
   python tools/pmc_summary.py profiles/r02/pmc_c1 [kernel_stats.csv]
 """
 import csv
+import statistics
 import sys
 from pathlib import Path
 
@@ -17,7 +18,8 @@ def main():
         for r in csv.DictReader(open(f)):
             if "trace_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"]:
                 acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    avg = {k: sum(v) / len(v) for k, v in acc.items()}
+    # the median launch, as bench.py takes it (the timed frames' recorded order)
+    avg = {k: statistics.median(v) for k, v in acc.items()}
     lines = [f"== {d}  (per-dispatch averages over the product kernel's launches)"]
     for k in sorted(avg):
         lines.append(f"  {k:26s} {avg[k]:.4g}")
