@@ -121,6 +121,10 @@ struct alignas(16) KArgs {
   int steal_min;
   int batch_max;                 // a wave's largest claim on a shared tile (0: by the pool)
   unsigned epoch;                // this launch's (per stream, 1 .. 65535)
+  // Drain compaction: a wave whose batches are spent and
+  // which holds at most `compact` paths posts them to its siblings through
+  // its traversal stack's LDS and leaves (0: off; <= kMbPaths(stack type))
+  int compact;
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -245,6 +249,16 @@ __device__ __forceinline__ bool xcas64(unsigned long long* p, unsigned long long
 // batches of 64 cost 1 % at one GPU, of 256 lose the balance at the tail;
 // profiles/r03/share_ab.txt)
 constexpr int kShareBatch = 128;
+// Drain compaction's mailbox: a donor wave writes its paths into its own
+// slice of the traversal stack ([entry][lane], dead between iterations):
+// field f of path p at entry row f / 2, in the (f & 1) half of the wave's
+// 64 entries of that row.  A donation holds as many paths as half a row
+// holds 32-bit words (16 with u16 entries, 8 with u8); its 13 fields take 7
+// rows, so the host enables it for stacks of at least 7 entries.
+constexpr int kMbFields = 13;
+constexpr int kMbRows = (kMbFields + 1) / 2;
+template <typename StackT>
+constexpr int kMbPaths = 8 * static_cast<int>(sizeof(StackT));
 __device__ __forceinline__ unsigned word_epoch(unsigned long long w) { return static_cast<unsigned>(w >> 48); }
 __device__ __forceinline__ int word_helpers(unsigned long long w) { return static_cast<int>((w >> 32) & 0xffffu); }
 // a workgroup-uniform value read from LDS, moved to a scalar register (an LDS
@@ -329,6 +343,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   __shared__ int s_unit[2];           // a helper's tile and first index
   __shared__ unsigned long long s_best;
   __shared__ int s_last;
+  // drain compaction: per wave the paths it posted and how many were taken;
+  // the waves still in the hot loop
+  __shared__ int s_mb_post[4], s_mb_take[4], s_alive, s_mb_avail;
+  // per wave: post when down to this many paths (0: posted once already; -1: off)
+  __shared__ int s_mb_lim[4];
   // A/B build only (-DRTCLJ_AB_RING): camera samples made in
   // per-wave batches into LDS rings.  Worth 2.6 % at 5 workgroups per CU,
   // but its 5 KB of LDS keep the default traversal from the sixth (§8)
@@ -503,6 +522,13 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     }
     s_join = own ? 0 : 1;
     s_pool_next = kRing ? 0 : 256;   // (the ring claims its own)
+    s_alive = 4;
+    s_mb_avail = 0;   // (posted, not yet taken: a hint for the waves' exits to the step)
+  }
+  if (threadIdx.x < 4) {
+    s_mb_post[threadIdx.x] = 0;
+    s_mb_take[threadIdx.x] = 0;
+    s_mb_lim[threadIdx.x] = ka->compact > 0 ? ka->compact : -1;
   }
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
@@ -526,6 +552,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   int wb = 0, we = 0;
   int j = first + static_cast<int>(threadIdx.x), q = 0, k = 0;
   bool active = kRing ? true : j < pool;
+  if (!active) j = -1;   // (no path: j < 0, also after the refill; compaction relies on it)
 
   // path state
   uint32_t st = 0;
@@ -661,7 +688,125 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     ring_take(__ballot(1), true);   // every lane's first sample
   }
 
-  while (active) {
+  // Drain compaction keeps every lane of a wave in the loop
+  // once its batches are spent (a lane without a path skips the body; the
+  // step after it may give it a path a sibling wave posted); the wave leaves
+  // when none of its lanes has one
+  constexpr bool kCompact = !kRing && is_bvh_scan(SCAN);
+  const int wv = static_cast<int>(threadIdx.x >> 6);
+  auto mb_word = [&](int d, int f, int p) -> uint32_t* {
+    constexpr int SZ = static_cast<int>(sizeof(StackT));
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_stack) + (f >> 1) * 256 * SZ + d * 64 * SZ +
+                                       (f & 1) * 32 * SZ + 4 * p);
+  };
+  auto lds_load = [](int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  // Once the wave's batches are spent (wave-uniform): with no path left it
+  // counts itself out of s_alive, or with a few it posts them (unless it has
+  // posted once before) and counts itself out; a wave that stays takes what
+  // the siblings posted into its free lanes.  Each post lands before its
+  // wave counts out, so a wave still counted in sees it; the last wave out
+  // finds every sibling gone -- it takes what is left, keeps its own paths,
+  // and counts itself back in.
+  auto compact_step = [&]() {
+    const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
+    const uint64_t live = __ballot(active);
+    const int left = static_cast<int>(__popcll(live));
+    bool out = false;   // counted out, and the last wave to do so
+    bool post = false;
+    if (left > 0 && left <= sgpr(lds_load(&s_mb_lim[wv]))) {
+      post = sgpr(lds_load(&s_alive)) > 1;
+      // posting now; or alone (no sibling will ever take them): not again
+      if (lane == leader) __hip_atomic_store(&s_mb_lim[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (left == 0 || post) {
+      if (post) {
+        const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(live >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(live), 0u)));
+        if (active) {
+          *mb_word(wv, 0, rank) = __float_as_uint(ox);
+          *mb_word(wv, 1, rank) = __float_as_uint(oy);
+          *mb_word(wv, 2, rank) = __float_as_uint(oz);
+          *mb_word(wv, 3, rank) = __float_as_uint(dx);
+          *mb_word(wv, 4, rank) = __float_as_uint(dy);
+          *mb_word(wv, 5, rank) = __float_as_uint(dz);
+          *mb_word(wv, 6, rank) = __float_as_uint(tr);
+          *mb_word(wv, 7, rank) = __float_as_uint(tg);
+          *mb_word(wv, 8, rank) = __float_as_uint(tb);
+          *mb_word(wv, 9, rank) = st;
+          *mb_word(wv, 10, rank) = static_cast<uint32_t>(q);
+          *mb_word(wv, 11, rank) = static_cast<uint32_t>(rem);
+          *mb_word(wv, 12, rank) = static_cast<uint32_t>(last);
+        }
+      }
+      int old = 0;
+      if (lane == leader) {
+        if (post) {
+          __hip_atomic_store(&s_mb_post[wv], left, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          atomicAdd(&s_mb_avail, left);
+        }
+        old = __hip_atomic_fetch_add(&s_alive, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the last one out withdraws its post (no sibling is left to take any of it)
+        if (post && old <= 1) {
+          __hip_atomic_store(&s_mb_post[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          atomicAdd(&s_mb_avail, -left);
+        }
+      }
+      old = __builtin_amdgcn_readlane(old, leader);
+      if (old > 1) {
+        active = false;   // (a post's paths are the siblings' now)
+        j = -1;
+        return;
+      }
+      out = true;
+    }
+    // free lanes take the siblings' posts, in rank order
+    uint64_t freem = ~live;
+    bool took = false;
+#pragma unroll 1
+    for (int d = 0; d < 4 && freem; ++d) {
+      if (d == wv) continue;
+      const int posted = sgpr(lds_load(&s_mb_post[d]));
+      if (posted <= sgpr(lds_load(&s_mb_take[d]))) continue;
+      const int want = static_cast<int>(__popcll(freem));
+      int t0 = 0;
+      if (lane == leader) t0 = atomicAdd(&s_mb_take[d], want);
+      t0 = __builtin_amdgcn_readlane(t0, leader);
+      const int got = min(want, posted - t0);
+      if (got <= 0) continue;
+      if (lane == leader) atomicAdd(&s_mb_avail, -got);
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(freem >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(freem), 0u)));
+      const bool mine = ((freem >> lane) & 1ull) && rank < got;
+      if (mine) {
+        const int p = t0 + rank;
+        ox = __uint_as_float(*mb_word(d, 0, p));
+        oy = __uint_as_float(*mb_word(d, 1, p));
+        oz = __uint_as_float(*mb_word(d, 2, p));
+        dx = __uint_as_float(*mb_word(d, 3, p));
+        dy = __uint_as_float(*mb_word(d, 4, p));
+        dz = __uint_as_float(*mb_word(d, 5, p));
+        tr = __uint_as_float(*mb_word(d, 6, p));
+        tg = __uint_as_float(*mb_word(d, 7, p));
+        tb = __uint_as_float(*mb_word(d, 8, p));
+        st = *mb_word(d, 9, p);
+        q = static_cast<int>(*mb_word(d, 10, p));
+        rem = static_cast<int>(*mb_word(d, 11, p));
+        last = static_cast<int>(*mb_word(d, 12, p));
+        active = true;
+        fresh = false;
+        j = 0;
+      }
+      freem &= ~__ballot(mine);
+      took = true;
+    }
+    // the last wave out stays in the loop if it has paths
+    if (out && (took || left > 0) && lane == leader) atomicAdd(&s_alive, 1);
+  };
+  // one segment of the wave's active lanes' paths, then their refill (the
+  // compaction exit clears every lane's `active`: the lanes keep their paths,
+  // j >= 0 tells them apart)
+  auto iteration = [&]() {
+    bool done = false;
     if constexpr (STATS) st_ts = stamp();
     if constexpr (STATS) {  // counted once per wave event, by its first active lane
       const uint64_t ex = __builtin_amdgcn_read_exec();
@@ -1167,7 +1312,6 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       st_c_scan += t - st_ts;
       st_ts = t;
     }
-    bool done = false;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f;
     if (best < 0) {
       // sky (raytracing.clj:55-58)
@@ -1355,6 +1499,35 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       }
     }
     if constexpr (STATS) st_c_acc += stamp() - st_ts;
+    if constexpr (kCompact) {
+      // spent: out to the compaction step when this wave may post its few
+      // paths, or its idle lanes may take posted ones
+      // (the limit and the flags from LDS: no registers held for them)
+      if (wb >= pool) {
+        const int lim = sgpr(lds_load(&s_mb_lim[threadIdx.x >> 6]));
+        if (lim >= 0) {
+          const int left = static_cast<int>(__popcll(__ballot(active)));
+          // (not while a lane holds a camera sample it has not started: no
+          // lane leaves the loop fresh, so that the step needs no fresh flags)
+          if ((left <= lim || (left < 64 && sgpr(lds_load(&s_mb_avail)) > 0)) && __ballot(active && fresh) == 0)
+            active = false;
+        }
+      }
+    }
+  };
+  for (;;) {
+    while (active) iteration();
+    if constexpr (!kCompact) {
+      break;
+    } else {
+      if (sgpr(lds_load(&s_mb_lim[wv])) < 0) break;   // (-1: compaction off)
+      // (every lane here: the wave-level state is made the same in all)
+      wb = we = pool;
+      active = j >= 0;   // (the loop's flags are not carried out of it)
+      fresh = false;
+      compact_step();
+      if (__ballot(active) == 0) break;
+    }
   }
 
   // ---- per-pixel mean (compute-pixel's accum / spp, raytracing.clj:155) ----
@@ -2096,6 +2269,12 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.bvh_stack = stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
+  // drain compaction: a donation is 16 paths (u16 stack entries) or 8 (u8) in
+  // the donor's first 7 stack rows (RTCLJ_COMPACT: at most that many; 0 off)
+  {
+    const int cap = v.scan == SCAN_BVHO ? 8 : 16;
+    a.compact = is_bvh_scan(v.scan) && a.bvh_stack >= kMbRows ? std::min(cap, env_int("RTCLJ_COMPACT", cap, 0)) : 0;
+  }
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
   const int th = tile_rows(v.scan);   // the variant's tile rows
   const int gx = (p->width + kTile - 1) / kTile, gy = (rows + th - 1) / th;

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     res = {lib: [] for lib in a.libs}
+    res_plain = {lib: [] for lib in a.libs}   # dispatch_order: the frame in plain tile order
     out = open(a.out, "a") if a.out else None
     for r in range(a.rounds):
         for lib in a.libs:
@@ -44,14 +45,21 @@ def main():
             line = json.loads(p.stdout.strip().splitlines()[-1])
             ms = line["kernel_ms_avg"]
             res[lib].append(ms)
-            print(f"round {r} {Path(lib).name:24s} kernel {ms:.3f} ms  {line['value']:.0f} Msamples/s", flush=True)
+            plain = (line.get("dispatch_order") or {}).get("kernel_ms")
+            if plain is not None:
+                res_plain[lib].append(plain)
+            print(f"round {r} {Path(lib).name:24s} kernel {ms:.3f} ms  plain order {plain}  "
+                  f"{line['value']:.0f} Msamples/s", flush=True)
             if out:
                 out.write(json.dumps({"round": r, "lib": Path(lib).name, "kernel_ms_avg": ms,
                                       "value": line["value"], "bvh": line.get("bvh_per_segment"),
+                                      "plain_ms": plain,
                                       "args": extra}) + "\n")
                 out.flush()
     for lib, v in res.items():
         print(f"{Path(lib).name:24s} median {statistics.median(v):.3f} ms  min {min(v):.3f}  runs {v}")
+        if res_plain[lib]:
+            print(f"{Path(lib).name:24s} plain order median {statistics.median(res_plain[lib]):.3f} ms")
 
 
 if __name__ == "__main__":
