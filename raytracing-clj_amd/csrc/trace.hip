@@ -692,7 +692,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // once its batches are spent (a lane without a path skips the body; the
   // step after it may give it a path a sibling wave posted); the wave leaves
   // when none of its lanes has one
+#ifdef RTCLJ_AB_NOCOMPACT
+  constexpr bool kCompact = false;   // (A/B build: the loop without compaction)
+#else
   constexpr bool kCompact = !kRing && is_bvh_scan(SCAN);
+#endif
   const int wv = static_cast<int>(threadIdx.x >> 6);
   auto mb_word = [&](int d, int f, int p) -> uint32_t* {
     constexpr int SZ = static_cast<int>(sizeof(StackT));
