@@ -453,20 +453,6 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # the same frame in plain dispatch order (no tile costs: what a launch of a
-    # new shape does), timed once after an untimed one, reported beside the
-    # timed, adaptively ordered steps
-    first_ms = None
-    if a.warmup > 0 and a.schedule == 0:
-        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        check(lib.rt_set_schedule(1))
-        step(0, p)
-        f0.record(stream)
-        step(0, p)
-        f1.record(stream)
-        torch.cuda.synchronize()
-        first_ms = f0.elapsed_time(f1)
-        check(lib.rt_set_schedule(a.schedule))
     # one frame at a time on one stream (no RT_FLAG_STREAMED): the kernel's
     # own duration, which the roofline and the rocprof average use
     single_ms = None
@@ -481,6 +467,32 @@ def main():
             e1.record(stream)
         torch.cuda.synchronize()
         single_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / n1
+    # a new shape's first launch (no tile costs yet: tiles in plain dispatch
+    # order, as a process's first frame runs), timed once the GPU is warm:
+    # after a launch of another shape (8 rows fewer), which makes this frame's
+    # shape new again; the second such pair is reported.  plain_ms: the same
+    # with the schedule off (rt_set_schedule(1)), for comparison
+    first_ms = plain_ms = None
+    if a.warmup > 0 and a.schedule == 0 and p.row_end - p.row_begin > 16:
+        other = type(p).from_buffer_copy(p)
+        other.row_end = p.row_end - 8
+        for _ in range(2):
+            step(0, other)
+            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g0.record(stream)
+            step(0, p)
+            g1.record(stream)
+            torch.cuda.synchronize()
+            first_ms = g0.elapsed_time(g1)
+        check(lib.rt_set_schedule(1))
+        step(0, p)
+        g0.record(stream)
+        step(0, p)
+        g1.record(stream)
+        torch.cuda.synchronize()
+        plain_ms = g0.elapsed_time(g1)
+        check(lib.rt_set_schedule(a.schedule))
+        step(0, p)   # (the record again, for the timed steps)
     for k in range(a.warmup * inflight):
         step(k)
     torch.cuda.synchronize()
@@ -508,7 +520,7 @@ def main():
             "kernel_ms_avg": single_ms if single_ms is not None else sum(kern_ms) / len(kern_ms),
             "launch_span_ms_avg": sum(kern_ms) / len(kern_ms),
             "kernel_ms_max": max(kern_ms), "rows": rows, "segments": cnt[0], "samples": cnt[1],
-            "first_launch_ms": first_ms, "ms_per_frame": elapsed / a.steps * 1e3}
+            "first_launch_ms": first_ms, "plain_ms": plain_ms, "ms_per_frame": elapsed / a.steps * 1e3}
     per_rank = [mine]
     if world > 1:
         per_rank = [None] * world
@@ -580,9 +592,12 @@ def main():
             "valu": valu, "occupancy": occ, "stats_build": stats,
             "kernel_ms_avg": kern_avg_ms, "launch_span_ms_max": mine["kernel_ms_max"],
             "dispatch_order": {"kernel_ms": mine["first_launch_ms"],
-                               "note": "the same frame with tiles in plain dispatch order (rt_set_schedule(1)), as a "
-                                       "launch of a new shape runs (no tile costs yet); the timed steps dispatch "
-                                       "longest first by the previous launches' per-tile durations (each added to half the record before it)"},
+                               "plain_schedule_off_ms": mine["plain_ms"],
+                               "note": "the first launch of a new shape (no tile costs yet: tiles in plain dispatch "
+                                       "order, as a process's first frame runs), timed after the GPU is warm, right "
+                                       "after a launch of another shape; plain_schedule_off_ms: the same frame with "
+                                       "the schedule off (rt_set_schedule(1)); the timed steps dispatch longest first by "
+                                       "the previous launches' per-tile durations (each added to half the record before it)"},
             "frames_in_flight": {"streams": inflight, "rt_launch_flags": "RT_FLAG_STREAMED" if inflight > 1 else 0,
                                  "launch_span_ms_avg": mine["launch_span_ms_avg"],
                                  "note": "timed frames go round-robin to this many streams (independent frames: "

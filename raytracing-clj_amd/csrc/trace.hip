@@ -256,6 +256,8 @@ constexpr int kShareBatch = 128;
 // holds 32-bit words (16 with u16 entries, 8 with u8); its 13 fields take 7
 // rows, so the host enables it for stacks of at least 7 entries.
 constexpr int kMbFields = 13;
+// stats builds / RTCLJ_TIMELINE: waves recorded per launch (dispatch slot order)
+constexpr int kDbgWaves = 1 << 17;
 constexpr int kMbRows = (kMbFields + 1) / 2;
 template <typename StackT>
 constexpr int kMbPaths = 8 * static_cast<int>(sizeof(StackT));
@@ -1645,7 +1647,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // the diagnostic build; NULL otherwise: a uniform branch)
   if (a.dbgw && lane == 0) {
     const size_t wid = static_cast<size_t>(unit) * 4 + (threadIdx.x >> 6);   // by dispatch slot
-    if (wid < 65536) {
+    if (wid < kDbgWaves) {
       a.dbgw[4 * wid + 0] = st_t0;
       a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
       a.dbgw[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -1810,7 +1812,7 @@ static const bool g_timeline = [] {
   return e && std::atoi(e) != 0;
 }();
 #endif
-// stats builds: per device, u64[kDbg] event counters and the u64[4 * 65536]
+// stats builds: per device, u64[kDbg] event counters and the u64[4 * kDbgWaves]
 // wave timeline, allocated on that device at its first stats launch
 constexpr int kDbg = 32;
 constexpr int kDbgDevices = 64;
@@ -2168,8 +2170,8 @@ static int dbg_buffers(int device, unsigned long long** dbg, unsigned long long*
   if (!g_dbg[device]) {
     HIP_TRY(hipMalloc(&g_dbg[device], kDbg * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(g_dbg[device], 0, kDbg * sizeof(unsigned long long)));
-    HIP_TRY(hipMalloc(&g_dbgw[device], 4 * 65536 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * 65536 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&g_dbgw[device], 4 * kDbgWaves * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * kDbgWaves * sizeof(unsigned long long)));
   }
   *dbg = g_dbg[device];
   *dbgw = g_dbgw[device];
@@ -2543,10 +2545,10 @@ extern "C" int rt_debug_waves(int device, uint64_t* out, size_t n_waves) {
   if (device < 0 || device >= kDbgDevices) return set_error(RT_E_ARG, "rt_debug_waves: bad device");
   std::lock_guard<std::mutex> lk(g_dbg_mu);
   if (!g_dbgw[device]) return 0;
-  if (n_waves > 65536) n_waves = 65536;
+  if (n_waves > kDbgWaves) n_waves = kDbgWaves;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, g_dbgw[device], 4 * n_waves * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * 65536 * sizeof(uint64_t)));
+  HIP_TRY(hipMemset(g_dbgw[device], 0, 4 * kDbgWaves * sizeof(uint64_t)));
   return static_cast<int>(n_waves);
 }

@@ -269,3 +269,4 @@ def test_streamed_frames_in_flight_are_bit_exact(env):
     from rtclj._lib import RTError
     with pytest.raises(RTError):
         R.render(sc, cam, 64, 36, spp=2, flags=RT_FLAG_STREAMED)
+

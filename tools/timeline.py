@@ -70,8 +70,8 @@ def main():
     torch.cuda.synchronize()
     st = (C.c_uint64 * 32)()
     check(lib.rt_debug_stats(st))
-    wv = np.zeros(4 * 65536, np.uint64)
-    check(lib.rt_debug_waves(0, wv.ctypes.data_as(C.POINTER(C.c_uint64)), 65536))
+    wv = np.zeros(4 * 131072, np.uint64)
+    check(lib.rt_debug_waves(0, wv.ctypes.data_as(C.POINTER(C.c_uint64)), 131072))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record(stream)
     launch()
@@ -79,7 +79,7 @@ def main():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e)
     check(lib.rt_debug_stats(st))
-    n = check(lib.rt_debug_waves(0, wv.ctypes.data_as(C.POINTER(C.c_uint64)), 65536))
+    n = check(lib.rt_debug_waves(0, wv.ctypes.data_as(C.POINTER(C.c_uint64)), 131072))
     w = wv[: 4 * n].reshape(n, 4).astype(np.int64)
     w = w[w[:, 1] > 0]
     t0 = w[:, 0].min()
