@@ -123,8 +123,9 @@ struct alignas(16) KArgs {
   unsigned epoch;                // this launch's (per stream, 1 .. 65535)
   // Drain compaction: a wave whose batches are spent and
   // which holds at most `compact` paths posts them to its siblings through
-  // its traversal stack's LDS and leaves (0: off; <= kMbPaths(stack type))
+  // its traversal stack's LDS and leaves (0: off; <= mb_paths)
   int compact;
+  int mb_paths;   // paths a post holds: as many as the wave's stack slice has room for (<= 32)
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -251,16 +252,13 @@ __device__ __forceinline__ bool xcas64(unsigned long long* p, unsigned long long
 constexpr int kShareBatch = 128;
 // Drain compaction's mailbox: a donor wave writes its paths into its own
 // slice of the traversal stack ([entry][lane], dead between iterations):
-// field f of path p at entry row f / 2, in the (f & 1) half of the wave's
-// 64 entries of that row.  A donation holds as many paths as half a row
-// holds 32-bit words (16 with u16 entries, 8 with u8); its 13 fields take 7
-// rows, so the host enables it for stacks of at least 7 entries.
+// word f * P + p (field f of path p, P paths per post) at entry row
+// (f * P + p) / W, word (f * P + p) % W of the wave's W = 16 x sizeof(entry)
+// words in that row.  P = as many as the slice holds, 13 fields each (C1's
+// depth-9 u16 stack: 22; at most 32).
 constexpr int kMbFields = 13;
 // stats builds / RTCLJ_TIMELINE: waves recorded per launch (dispatch slot order)
 constexpr int kDbgWaves = 1 << 17;
-constexpr int kMbRows = (kMbFields + 1) / 2;
-template <typename StackT>
-constexpr int kMbPaths = 8 * static_cast<int>(sizeof(StackT));
 __device__ __forceinline__ unsigned word_epoch(unsigned long long w) { return static_cast<unsigned>(w >> 48); }
 __device__ __forceinline__ int word_helpers(unsigned long long w) { return static_cast<int>((w >> 32) & 0xffffu); }
 // a workgroup-uniform value read from LDS, moved to a scalar register (an LDS
@@ -700,10 +698,12 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   constexpr bool kCompact = !kRing && is_bvh_scan(SCAN);
 #endif
   const int wv = static_cast<int>(threadIdx.x >> 6);
-  auto mb_word = [&](int d, int f, int p) -> uint32_t* {
+  auto mb_word = [&](int d, int f, int p, int P) -> uint32_t* {
     constexpr int SZ = static_cast<int>(sizeof(StackT));
-    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_stack) + (f >> 1) * 256 * SZ + d * 64 * SZ +
-                                       (f & 1) * 32 * SZ + 4 * p);
+    constexpr int W = 16 * SZ;   // words per stack row per wave
+    const int i = f * P + p;
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_stack) + (i / W) * 256 * SZ + d * 64 * SZ +
+                                       (i % W) * 4);
   };
   auto lds_load = [](int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
   // Once the wave's batches are spent (wave-uniform): with no path left it
@@ -714,6 +714,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // finds every sibling gone -- it takes what is left, keeps its own paths,
   // and counts itself back in.
   auto compact_step = [&]() {
+    const int P = kargs_opaque()->mb_paths;
     const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
     const uint64_t live = __ballot(active);
     const int left = static_cast<int>(__popcll(live));
@@ -729,19 +730,19 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(live >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(live), 0u)));
         if (active) {
-          *mb_word(wv, 0, rank) = __float_as_uint(ox);
-          *mb_word(wv, 1, rank) = __float_as_uint(oy);
-          *mb_word(wv, 2, rank) = __float_as_uint(oz);
-          *mb_word(wv, 3, rank) = __float_as_uint(dx);
-          *mb_word(wv, 4, rank) = __float_as_uint(dy);
-          *mb_word(wv, 5, rank) = __float_as_uint(dz);
-          *mb_word(wv, 6, rank) = __float_as_uint(tr);
-          *mb_word(wv, 7, rank) = __float_as_uint(tg);
-          *mb_word(wv, 8, rank) = __float_as_uint(tb);
-          *mb_word(wv, 9, rank) = st;
-          *mb_word(wv, 10, rank) = static_cast<uint32_t>(q);
-          *mb_word(wv, 11, rank) = static_cast<uint32_t>(rem);
-          *mb_word(wv, 12, rank) = static_cast<uint32_t>(last);
+          *mb_word(wv, 0, rank, P) = __float_as_uint(ox);
+          *mb_word(wv, 1, rank, P) = __float_as_uint(oy);
+          *mb_word(wv, 2, rank, P) = __float_as_uint(oz);
+          *mb_word(wv, 3, rank, P) = __float_as_uint(dx);
+          *mb_word(wv, 4, rank, P) = __float_as_uint(dy);
+          *mb_word(wv, 5, rank, P) = __float_as_uint(dz);
+          *mb_word(wv, 6, rank, P) = __float_as_uint(tr);
+          *mb_word(wv, 7, rank, P) = __float_as_uint(tg);
+          *mb_word(wv, 8, rank, P) = __float_as_uint(tb);
+          *mb_word(wv, 9, rank, P) = st;
+          *mb_word(wv, 10, rank, P) = static_cast<uint32_t>(q);
+          *mb_word(wv, 11, rank, P) = static_cast<uint32_t>(rem);
+          *mb_word(wv, 12, rank, P) = static_cast<uint32_t>(last);
         }
       }
       int old = 0;
@@ -785,19 +786,19 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       const bool mine = ((freem >> lane) & 1ull) && rank < got;
       if (mine) {
         const int p = t0 + rank;
-        ox = __uint_as_float(*mb_word(d, 0, p));
-        oy = __uint_as_float(*mb_word(d, 1, p));
-        oz = __uint_as_float(*mb_word(d, 2, p));
-        dx = __uint_as_float(*mb_word(d, 3, p));
-        dy = __uint_as_float(*mb_word(d, 4, p));
-        dz = __uint_as_float(*mb_word(d, 5, p));
-        tr = __uint_as_float(*mb_word(d, 6, p));
-        tg = __uint_as_float(*mb_word(d, 7, p));
-        tb = __uint_as_float(*mb_word(d, 8, p));
-        st = *mb_word(d, 9, p);
-        q = static_cast<int>(*mb_word(d, 10, p));
-        rem = static_cast<int>(*mb_word(d, 11, p));
-        last = static_cast<int>(*mb_word(d, 12, p));
+        ox = __uint_as_float(*mb_word(d, 0, p, P));
+        oy = __uint_as_float(*mb_word(d, 1, p, P));
+        oz = __uint_as_float(*mb_word(d, 2, p, P));
+        dx = __uint_as_float(*mb_word(d, 3, p, P));
+        dy = __uint_as_float(*mb_word(d, 4, p, P));
+        dz = __uint_as_float(*mb_word(d, 5, p, P));
+        tr = __uint_as_float(*mb_word(d, 6, p, P));
+        tg = __uint_as_float(*mb_word(d, 7, p, P));
+        tb = __uint_as_float(*mb_word(d, 8, p, P));
+        st = *mb_word(d, 9, p, P);
+        q = static_cast<int>(*mb_word(d, 10, p, P));
+        rem = static_cast<int>(*mb_word(d, 11, p, P));
+        last = static_cast<int>(*mb_word(d, 12, p, P));
         active = true;
         fresh = false;
         j = 0;
@@ -2275,11 +2276,12 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.bvh_stack = stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
-  // drain compaction: a donation is 16 paths (u16 stack entries) or 8 (u8) in
-  // the donor's first 7 stack rows (RTCLJ_COMPACT: at most that many; 0 off)
+  // drain compaction: a post holds as many paths as a wave's stack slice has
+  // room for (RTCLJ_COMPACT: post at or below that many paths; 0 off)
   {
-    const int cap = v.scan == SCAN_BVHO ? 8 : 16;
-    a.compact = is_bvh_scan(v.scan) && a.bvh_stack >= kMbRows ? std::min(cap, env_int("RTCLJ_COMPACT", cap, 0)) : 0;
+    const int words = a.bvh_stack * 16 * (v.scan == SCAN_BVHO ? 1 : 2);   // a wave's stack slice
+    a.mb_paths = std::min(32, words / kMbFields);
+    a.compact = is_bvh_scan(v.scan) ? std::min(a.mb_paths, env_int("RTCLJ_COMPACT", a.mb_paths, 0)) : 0;
   }
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
   const int th = tile_rows(v.scan);   // the variant's tile rows
