@@ -7,7 +7,7 @@ leaves) and the colour sums are integers, so every frame must equal the
 oracle's fp32 mirror (MODE_MIRROR32) bit for bit whoever finishes which
 path -- at every threshold, with and without tile sharing and sample splits,
 on pools smaller than a workgroup's 256 lanes (fewer waves start) and on
-C4's 8-body-leaf traversal (u8 stack: 8 paths per post).
+C4's 8-body-leaf traversal (u8 stack: smaller posts).
 """
 import ctypes as C
 
@@ -48,13 +48,14 @@ def cover(gpu_lib):
     lib.rt_scene_free(ds)
 
 
-@pytest.mark.parametrize("knobs", [dict(RTCLJ_COMPACT="16"), dict(RTCLJ_COMPACT="1"),
+@pytest.mark.parametrize("knobs", [dict(RTCLJ_COMPACT="64"), dict(RTCLJ_COMPACT="16"), dict(RTCLJ_COMPACT="1"),
                                    dict(RTCLJ_COMPACT="5", RTCLJ_SPLIT="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_SPLIT="1", RTCLJ_STEAL_MIN="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_STEAL="0"),
                                    dict(RTCLJ_COMPACT="0")])
 def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
-    """Thresholds 16 (a whole post), 1 and 5; tiles kept whole and shared
+    """Thresholds 64 (clamped: posts as full as the stack slice holds, 22 on
+    this scene's tree), 16, 1 and 5; tiles kept whole and shared
     (RTCLJ_SPLIT=1, helpers joining any tile), sharing off, compaction off;
     frames of many small pools, few large ones (sample splits by default) and
     pools of 1..255 samples: each launched twice (plain order, then the
@@ -73,9 +74,9 @@ def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
 
 
 def test_compaction_on_the_eight_body_leaf_traversal(gpu_lib, monkeypatch):
-    """C4's 1000-body scene runs the 8-body-leaf tree with a u8 stack (posts
-    of 8 paths): a strip at depth 64 equals the mirror with compaction on
-    (the default) and at threshold 3."""
+    """C4's 1000-body scene runs the 8-body-leaf tree with a u8 stack (half
+    the room per post): a strip at depth 64 equals the mirror with
+    compaction on (the default) and at threshold 3."""
     from rtclj import scenes
     from rtclj._lib import check, lib
     sc = scenes.cover_c4()
