@@ -552,7 +552,12 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   int wb = 0, we = 0;
   int j = first + static_cast<int>(threadIdx.x), q = 0, k = 0;
   bool active = kRing ? true : j < pool;
-  if (!active) j = -1;   // (no path: j < 0, also after the refill; compaction relies on it)
+  // With compaction (kCompact, below) j is the lane's whole state in the
+  // loop: j >= 0 a sample not started yet (pool index j), -1 a path in
+  // progress, -2 no path, -3 a path taken out of the loop to the
+  // compaction step; the loop carries no flag (one live across the step
+  // would be a VGPR 0/1 tested every iteration)
+  if (!active) j = -2;
 
   // path state
   uint32_t st = 0;
@@ -761,7 +766,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       old = __builtin_amdgcn_readlane(old, leader);
       if (old > 1) {
         active = false;   // (a post's paths are the siblings' now)
-        j = -1;
+        j = -2;
         return;
       }
       out = true;
@@ -801,7 +806,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         last = static_cast<int>(*mb_word(d, 12, p, P));
         active = true;
         fresh = false;
-        j = 0;
+        j = -1;
       }
       freem &= ~__ballot(mine);
       took = true;
@@ -809,9 +814,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     // the last wave out stays in the loop if it has paths
     if (out && (took || left > 0) && lane == leader) atomicAdd(&s_alive, 1);
   };
-  // one segment of the wave's active lanes' paths, then their refill (the
-  // compaction exit clears every lane's `active`: the lanes keep their paths,
-  // j >= 0 tells them apart)
+  // one segment of the wave's active lanes' paths, then their refill (with
+  // compaction, j's states above; `active` and `fresh` are only the step's and
+  // the other variants')
   auto iteration = [&]() {
     bool done = false;
     if constexpr (STATS) st_ts = stamp();
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         st_lanes += __popcll(ex);
       }
     }
-    if (fresh) {
+    if (kCompact ? j >= 0 : fresh) {
       if constexpr (STATS) {
         const uint64_t ex = __builtin_amdgcn_read_exec();
         if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -886,6 +891,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       rem = a.max_depth;
       last = -1;
       fresh = false;
+      if constexpr (kCompact) j = -1;
     }
 
 
@@ -1500,7 +1506,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         if (wb >= pool) we = pool;   // spent: the lanes left over retire
       }
       if (done) {
-        j = nj;
+        j = kCompact && nj < 0 ? -2 : nj;
         fresh = true;
         if (nj < 0) active = false;
       }
@@ -1513,25 +1519,30 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       if (wb >= pool) {
         const int lim = sgpr(lds_load(&s_mb_lim[threadIdx.x >> 6]));
         if (lim >= 0) {
-          const int left = static_cast<int>(__popcll(__ballot(active)));
+          const int left = static_cast<int>(__popcll(__ballot(j >= -1)));
           // (not while a lane holds a camera sample it has not started: no
           // lane leaves the loop fresh, so that the step needs no fresh flags)
-          if ((left <= lim || (left < 64 && sgpr(lds_load(&s_mb_avail)) > 0)) && __ballot(active && fresh) == 0)
-            active = false;
+          if ((left <= lim || (left < 64 && sgpr(lds_load(&s_mb_avail)) > 0)) && __ballot(j >= 0) == 0 &&
+              j == -1)
+            j = -3;   // (out of the loop, the path kept)
         }
       }
     }
   };
   for (;;) {
-    while (active) iteration();
+    if constexpr (kCompact) {
+      while (j >= -1) iteration();
+    } else {
+      while (active) iteration();
+    }
     if constexpr (!kCompact) {
       break;
     } else {
       if (sgpr(lds_load(&s_mb_lim[wv])) < 0) break;   // (-1: compaction off)
       // (every lane here: the wave-level state is made the same in all)
       wb = we = pool;
-      active = j >= 0;   // (the loop's flags are not carried out of it)
-      fresh = false;
+      active = j == -3;   // the lanes that left the loop with a path
+      if (active) j = -1;
       compact_step();
       if (__ballot(active) == 0) break;
     }
