@@ -122,19 +122,26 @@ def camera(image_width, image_h, vfov, look_from, look_at, vup, defocus_angle, f
 
 def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50, seed: int = 1,
            n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None,
-           flags: int = 0, library=None):
+           flags: int = 0, library=None, out=None):
     """compute-pixel for every pixel of rows [r0, r1) (default: all), on the GPU.
 
     Returns float32 (rows, width, 3) linear RGB, each pixel the mean of its spp
     samples (raytracing.clj:155).  `scene` is a Scene or a list of bodies.
-    `library`: another loaded build of the ABI (rtclj._lib.diag_lib())."""
+    `library`: another loaded build of the ABI (rtclj._lib.diag_lib()).
+    `out`: a C-contiguous float32 (rows, width, 3) array to render into (a
+    renderer drawing frames reuses its framebuffer; a fresh 10 MB array's
+    pages are first touched by the copy into it)."""
     dll = library if library is not None else lib
     if not isinstance(scene, Scene):
         scene = Scene.from_bodies(scene)
     r0, r1 = (0, height) if rows is None else rows
     p = rt_params(width=width, height=height, row_begin=r0, row_end=r1, spp=spp, max_depth=max_depth,
                   seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
-    out = np.empty((max(r1 - r0, 0), width, 3), np.float32)
+    shape = (max(r1 - r0, 0), width, 3)
+    if out is None:
+        out = np.empty(shape, np.float32)
+    elif out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
+        raise ValueError(f"render: out must be C-contiguous float32 {shape}")
     st = rt_stats()
     code = dll.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st))
     if code < 0:

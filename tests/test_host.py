@@ -90,3 +90,17 @@ def test_shard_plans_cover_frame_once():
         gather_rows(4, 1, [([0, 1], np.zeros((2, 1, 3))), ([1, 2, 3], np.zeros((3, 1, 3)))])
     with pytest.raises(ValueError):
         shard_params(2, 2, 1, 1, 1, 1)
+
+
+def test_render_out_buffer_is_checked_before_any_device_call():
+    """render(out=...) reuses a caller framebuffer: the wrong shape, dtype or
+    layout is refused before the library is called (no GPU needed)."""
+    import numpy as np
+    import pytest
+    from rtclj import raytracing as R, scenes
+    sc = scenes.cover(11)
+    cam = scenes.cover_camera(64, 36)
+    for bad in (np.empty((36, 64, 3), np.float64), np.empty((35, 64, 3), np.float32),
+                np.empty((64, 36, 3), np.float32).transpose(1, 0, 2)):
+        with pytest.raises(ValueError):
+            R.render(sc, cam, 64, 36, 1, 50, out=bad)
