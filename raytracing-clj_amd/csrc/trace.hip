@@ -13,7 +13,10 @@
 //     (pixel, sample) pair of it: the *sample pool*.  A lane runs one path
 //     at a time; when it ends (sky / absorbed / depth) the lane hands in its
 //     colour and takes the next pair from an LDS counter, so no lane idles
-//     until the pool is empty;
+//     until the pool is empty; then a wave down to its last few paths hands
+//     them to its sibling waves' idle lanes (drain compaction) and leaves;
+//   * a launch's last tiles are shared with helper workgroups dispatched in
+//     its tail (tile sharing), and launches of few tiles split their samples;
 //   * ray-color's recursion becomes a throughput accumulator T (stackless);
 //   * the closest hit comes from a BVH in LDS (default) or, in the fallback
 //     and diagnostic variants, a linear scan of the sphere table (LDS or the
