@@ -50,7 +50,8 @@ typedef enum rt_status {
   RT_E_TOO_MANY = -3,   /* sphere list larger than the LDS-resident limit        */
   RT_E_HIP = -4,        /* HIP runtime error (message has the HIP error string)  */
   RT_E_NODEV = -5,      /* no GPU visible / device index out of range            */
-  RT_E_IO = -6          /* file I/O (rt_write_ppm, rt_write_png, rt_ppm_to_png)  */
+  RT_E_IO = -6,         /* file I/O (rt_write_ppm, rt_write_png, rt_ppm_to_png)  */
+  RT_E_ALLOC = -7       /* host memory exhausted (the JNI shim's frame buffer)   */
 } rt_status;
 
 /* ---- material kinds: material.clj:13 (lambertian), :21 (metal), :34 (dielectric).

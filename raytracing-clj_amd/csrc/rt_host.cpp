@@ -130,16 +130,32 @@ extern "C" int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int
   if (!path || !rgb || width <= 0 || height <= 0) return set_error(RT_E_ARG, "rt_write_ppm: bad argument");
   FILE* f = std::fopen(path, "wb");
   if (!f) return set_error(RT_E_IO, std::string("rt_write_ppm: cannot open ") + path);
-  std::string buf;
-  buf.reserve(static_cast<size_t>(width) * height * 12 + 32);
-  buf += "P3\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
-  char line[16];
+  // "r g b\n" per pixel (raytracing.clj:172-175) from a table of the 256
+  // decimal strings, each with its separator: no formatting per value (C1's
+  // 810,000 pixels: 41.7 ms with a snprintf each)
+  struct Dec {
+    char s[4];
+    int len;
+  };
+  static const auto* const dec = [] {
+    auto* t = new Dec[256];
+    for (int v = 0; v < 256; ++v) t[v].len = std::snprintf(t[v].s, sizeof t[v].s, "%d", v);
+    return t;
+  }();
+  const std::string head = "P3\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
   const size_t npx = static_cast<size_t>(width) * height;
-  for (size_t i = 0; i < npx; ++i) {
-    const int len = std::snprintf(line, sizeof line, "%d %d %d\n", rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]);
-    buf.append(line, len);
+  std::vector<char> buf(head.size() + npx * 12);   // at most "255 255 255\n" a pixel
+  char* o = buf.data();
+  std::memcpy(o, head.data(), head.size());
+  o += head.size();
+  for (size_t i = 0; i < 3 * npx; ++i) {
+    const Dec& d = dec[rgb[i]];
+    std::memcpy(o, d.s, 4);   // (the table entry's 4 bytes; the separator overwrites what follows the digits)
+    o += d.len;
+    *o++ = (i % 3 == 2) ? '\n' : ' ';
   }
-  const bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+  const size_t nb = static_cast<size_t>(o - buf.data());
+  const bool ok = std::fwrite(buf.data(), 1, nb, f) == nb;
   std::fclose(f);
   return ok ? RT_OK : set_error(RT_E_IO, std::string("rt_write_ppm: short write to ") + path);
 }
@@ -202,8 +218,12 @@ bool same_scene(const CachedScene& c, const rt_scene& s) {
 // ---- per-device render context: stream, buffers, events ---------------------
 struct Ctx {
   int device = 0;
-  // the device's NULL stream (its first context: creating a stream takes
-  // 5-7 ms on MI355X, tools/first_call.cpp -- most of a first call's set-up)
+  // the device's NULL stream: the first call of a device only (creating a
+  // stream takes 5-7 ms on MI355X, tools/first_call.cpp -- most of a first
+  // call's set-up).  The NULL stream synchronises with every blocking stream
+  // of the device (a host application's, synchronous copies), so the next
+  // call that takes this context gives it a non-blocking stream of its own
+  // (take_ctx), with the tile orders recorded so far.
   bool null_stream = false;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
@@ -211,11 +231,16 @@ struct Ctx {
   size_t d_cap = 0;           // floats
   uint64_t* d_cnt = nullptr;
   uint64_t* h_cnt = nullptr;  // pinned
+  std::vector<const void*> scenes;   // device scenes launched on (their per-stream schedule entries)
+  void launched(const void* ds) {
+    if (std::find(scenes.begin(), scenes.end(), ds) == scenes.end()) scenes.push_back(ds);
+  }
   ~Ctx() {
     (void)hipSetDevice(device);
     if (stream || null_stream) {
       (void)hipStreamSynchronize(stream);
-      release_stream_schedules(device, stream);   // the scenes' per-stream slots
+      // the per-stream slots of the scenes this context launched on
+      release_stream_schedules(stream, scenes.data(), static_cast<int>(scenes.size()));
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -311,7 +336,7 @@ int get_scene(int device, const rt_scene* s, std::shared_ptr<rt_dscene>* out, bo
 std::unique_ptr<Ctx> take_ctx(int device) {
   DeviceCache& dc = (*g_cache)[device];
   {
-    std::lock_guard<std::mutex> lk(dc.mu);
+    std::unique_lock<std::mutex> lk(dc.mu);
     if (!dc.primary_made) {   // the first context of the device: its NULL stream
       dc.primary_made = true;
       auto c = std::make_unique<Ctx>();
@@ -319,7 +344,20 @@ std::unique_ptr<Ctx> take_ctx(int device) {
       c->null_stream = true;
       return c;
     }
-    if (dc.primary) return std::move(dc.primary);
+    if (dc.primary) {
+      // its second use: off the NULL stream, onto a non-blocking stream of its
+      // own, keeping the tile orders the NULL stream's launches recorded (if
+      // the stream cannot be made, the context stays on the NULL stream)
+      std::unique_ptr<Ctx> c = std::move(dc.primary);
+      lk.unlock();
+      hipStream_t s = nullptr;
+      if (hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+        rebind_stream_schedules(nullptr, s, c->scenes.data(), static_cast<int>(c->scenes.size()));
+        c->stream = s;
+        c->null_stream = false;
+      }
+      return c;
+    }
     if (!dc.free_ctx.empty()) {
       std::unique_ptr<Ctx> c = std::move(dc.free_ctx.back());
       dc.free_ctx.pop_back();
@@ -414,6 +452,7 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
   if (e != hipSuccess) {
     hip_fail(e, "rt_render setup");
   } else {
+    cx->launched(ds.get());   // (before the launch: it may have made the stream's entry and then failed)
     rc = rt_launch(ds.get(), c, &sh->p, cx->d_out, cx->d_cnt, cx->stream);
     if (rc != RT_OK) {
       fail(rc);

@@ -36,8 +36,14 @@ int rows_out(const rt_params& p);
 
 // rt_render's contexts own their streams: before one destroys its stream
 // (already synchronised) it drops that stream's adaptive-schedule and
-// split-sum entries from every live device scene of `device` (trace.hip), so
-// the scenes' per-stream slots do not fill up with dead streams.
-void release_stream_schedules(int device, void* stream);
+// split-sum entries from the device scenes it launched on (`scenes`, n of
+// them; those no longer live are skipped), so the scenes' per-stream slots do
+// not fill up with dead streams -- and a direct rt_launch user's entries on a
+// stream the context shared (the NULL stream) are left alone (trace.hip).
+void release_stream_schedules(void* stream, const void* const* scenes, int n);
+// A context that moves from the NULL stream to a stream of its own keeps its
+// adaptive tile orders: the entries of `from` in those scenes become `to`'s
+// (both streams idle; a scene that already has an entry for `to` keeps it).
+void rebind_stream_schedules(void* from, void* to, const void* const* scenes, int n);
 
 }  // namespace rtclj

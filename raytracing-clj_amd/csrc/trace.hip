@@ -1590,6 +1590,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       const unsigned mine = static_cast<unsigned>(s_cnt);
       const unsigned prev = __hip_atomic_fetch_add(&ke->done[tile], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = prev + mine == static_cast<unsigned>(pool);
+      // the participant that completes the pool pairs the others' release
+      // fences with an acquire before it reads (and resets) the sums
+      if (prev + mine == static_cast<unsigned>(pool)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     if (sgpr(s_last)) {   // (every participant has added: the slots and done are free for the next use)
@@ -1877,7 +1880,8 @@ struct Schedule {
   int* owner = nullptr;                 // KArgs n_owner entries
   int owner_cap = 0;
   unsigned long long* stealc = nullptr; // [helpers that got samples, their first samples] since rt_steal_stats
-  unsigned epoch = 0;                   // launches with sharing on this stream
+  unsigned epoch = 0;                   // launches with sharing on this stream (mod 2^16, 1 .. 65535)
+  bool epoch_started = false;
 };
 constexpr int kSchedStreams = 8;
 struct ScheduleSet {
@@ -1932,13 +1936,30 @@ struct rt_dscene {
 static std::mutex g_scenes_mu;
 static std::vector<rt_dscene*> g_scenes;
 
-void rtclj::release_stream_schedules(int device, void* stream) {
+// the live scenes among `scenes` (a context's list may name freed ones)
+template <class F>
+static void for_live_scenes(const void* const* scenes, int n, F f) {
   std::lock_guard<std::mutex> lk(g_scenes_mu);
   for (rt_dscene* d : g_scenes)
-    if (d->device == device) {
+    if (std::find(scenes, scenes + n, static_cast<const void*>(d)) != scenes + n) {
       std::lock_guard<std::mutex> l2(d->sched.mu);
-      d->sched.release_stream(static_cast<hipStream_t>(stream));
+      f(d->sched);
     }
+}
+
+void rtclj::release_stream_schedules(void* stream, const void* const* scenes, int n) {
+  for_live_scenes(scenes, n, [&](ScheduleSet& set) { set.release_stream(static_cast<hipStream_t>(stream)); });
+}
+
+void rtclj::rebind_stream_schedules(void* from, void* to, const void* const* scenes, int n) {
+  for_live_scenes(scenes, n, [&](ScheduleSet& set) {
+    Schedule* src = nullptr;
+    for (int k = 0; k < set.used; ++k) {
+      if (set.s[k].stream == static_cast<hipStream_t>(to)) return;
+      if (set.s[k].stream == static_cast<hipStream_t>(from)) src = &set.s[k];
+    }
+    if (src) src->stream = static_cast<hipStream_t>(to);
+  });
 }
 
 static int hip_fail(hipError_t e, const char* what) {
@@ -2467,15 +2488,24 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch->owner_cap = n_owner;
       new_shape = true;
     }
+    if (!sch->epoch_started) {   // (RTCLJ_EPOCH_START: tests start a stream near the wrap)
+      sch->epoch = static_cast<unsigned>(std::min(0xffff, env_int("RTCLJ_EPOCH_START", 1, 1)) - 1);
+      sch->epoch_started = true;
+    }
     sch->epoch = (sch->epoch + 1) & 0xffffu;
-    if (sch->epoch == 0) {   // wrapped: no owner entry may name a word of the epoch's last use
+    if (sch->epoch == 0) {   // wrapped: no word or owner entry may carry the epoch's last use
       sch->epoch = 1;
       new_shape = true;
     }
     a.epoch = sch->epoch;
-    // a new shape: no tile is being run (old entries would only name words
-    // of other epochs, but tile indices of another shape may exceed this one's)
-    if (new_shape) HIP_TRY(hipMemsetAsync(sch->owner, 0xff, n_owner * sizeof(int), stream));
+    // a new shape (or a wrap): no tile is being run, and no word holds this
+    // launch's epoch.  (Old owner entries would only name words of other
+    // epochs, but tile indices of another shape may exceed this one's; a word
+    // last published 65,535 launches ago carries the epoch a wrap reuses.)
+    if (new_shape) {
+      HIP_TRY(hipMemsetAsync(sch->owner, 0xff, n_owner * sizeof(int), stream));
+      HIP_TRY(hipMemsetAsync(sch->word, 0, n_tiles * sizeof(unsigned long long), stream));
+    }
     a.word = sch->word;
     a.done = sch->done;
     a.sum = sch->sum;

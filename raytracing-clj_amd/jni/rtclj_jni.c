@@ -77,7 +77,13 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   if (!(mat = (float*)(*env)->GetFloatArrayElements(env, mats, NULL))) goto done;
   (*env)->GetFloatArrayRegion(env, camera, 0, 18, cam18);
   if ((*env)->ExceptionCheck(env)) goto done;
-  if (!(out = (float*)malloc(frame * sizeof(float)))) goto done;
+  if (!(out = (float*)malloc(frame * sizeof(float)))) {
+    /* out of memory, not a bad argument: java.lang.OutOfMemoryError */
+    jclass oom = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (oom) (*env)->ThrowNew(env, oom, "rtclj render: cannot allocate the frame buffer");
+    rc = RT_E_ALLOC;
+    goto done;
+  }
   rt_camera cam;
   memcpy(cam.center, cam18 + 0, 12);
   memcpy(cam.p00, cam18 + 3, 12);

@@ -111,3 +111,40 @@ def test_forced_sharing_is_bit_exact(env, monkeypatch, knobs):
             steals += st[0]
         if spp >= 40 and knobs == dict(RTCLJ_STEAL_MIN="1"):   # (2 batches of 256 < every such pool)
             assert steals > 0, (w, h, spp)
+
+
+def test_epoch_wrap_keeps_shared_tiles_exact(env, monkeypatch):
+    """The 16-bit launch epoch of a stream's tile words wraps after 65,535
+    sharing launches: rt_launch then re-zeroes the words and the owner table
+    (trace.hip, the epoch's set-up), so no word left by a launch 65,535
+    earlier looks current.  The stream's epoch starts at 65,528
+    (RTCLJ_EPOCH_START) and 16 launches cross the wrap, alternating spp on
+    one shape (the stale-owner race of a helper joining a tile published
+    with another spp) and shapes, with helpers joining any tile: every frame
+    equals the mirror, with no NaN (an unwritten tile)."""
+    from rtclj import scenes
+    from rtclj._lib import check, lib, rt_params
+    sc, _, torch = env
+    monkeypatch.setenv("RTCLJ_EPOCH_START", "65528")
+    monkeypatch.setenv("RTCLJ_STEAL_MIN", "1")
+    ds = C.c_void_p()   # a fresh scene: its stream entries start at the knob's epoch
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    try:
+        s = torch.cuda.Stream()
+        cases = [(24, 16, 600), (24, 16, 100), (24, 16, 300), (40, 24, 120)]
+        want = {}
+        for w, h, spp in cases:
+            want[(w, h, spp)] = _mirror(sc, scenes.cover_camera(w, h), w, h, spp, 9)
+        steals = 0
+        for k in range(16):
+            w, h, spp = cases[k % 3] if k % 5 != 4 else cases[3]
+            cam = scenes.cover_camera(w, h)
+            p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=50, seed=9)
+            got, st = _launch((sc, ds, torch), cam, p, s)
+            assert not np.isnan(got).any(), (k, w, h, spp)
+            assert np.array_equal(got, want[(w, h, spp)]), (k, w, h, spp)
+            steals += st[0]
+        assert steals > 0
+    finally:
+        torch.cuda.synchronize()
+        lib.rt_scene_free(ds)

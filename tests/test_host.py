@@ -73,6 +73,22 @@ def test_ppm_round_trip(tmp_path):
     assert np.array_equal(R.read_ppm(p), img)
 
 
+def test_ppm_bytes_equal_per_value_formatting(tmp_path):
+    """rt_write_ppm's table of decimal strings writes the bytes a "%d %d %d\\n"
+    per pixel would (raytracing.clj:172-175): every value 0..255, and a frame
+    of C1's width."""
+    from rtclj import raytracing as R
+    vals = np.arange(256, dtype=np.uint8)
+    rng = np.random.default_rng(1)
+    for img in (np.stack([vals, vals[::-1], np.roll(vals, 7)], -1).reshape(16, 16, 3),
+                rng.integers(0, 256, (9, 1200, 3)).astype(np.uint8)):
+        p = tmp_path / "v.ppm"
+        R.write_ppm(p, img)
+        h, w = img.shape[:2]
+        want = f"P3\n{w} {h}\n255\n" + "".join(f"{r} {g} {b}\n" for r, g, b in img.reshape(-1, 3).tolist())
+        assert p.read_bytes() == want.encode()
+
+
 def test_shard_plans_cover_frame_once():
     from rtclj.shard import gather_rows, shard_params, shard_rows
     h, w = 675, 3
