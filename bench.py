@@ -87,12 +87,15 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (rt_set_variant; 0 = default)")
     ap.add_argument("--schedule", type=int, default=0,
                     help="tile schedule (rt_set_schedule): 0 adaptive longest-first, 1 plain dispatch order")
-    ap.add_argument("--inflight", type=int, default=None,
-                    help="frames in flight: consecutive frames go round-robin to this many streams "
-                         "(rt_launch RT_FLAG_STREAMED when > 1); 1 = one stream, one frame at a time. "
-                         "Default: 1 on one GPU (each timed frame is one kernel, so the rocprof kernel "
-                         "durations are the frame times; a second stream gains ~1 %% there), 2 on several "
-                         "(a shard's frame is ~1 ms: the next frame fills its tail, DESIGN.md §6)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames in flight of the timed steps that make `value`: consecutive frames go "
+                         "round-robin to this many streams (rt_launch RT_FLAG_STREAMED when > 1); 1 (default, "
+                         "at every N) = one stream, one frame at a time, so `value` is single-frame throughput "
+                         "at every N and the rocprof kernel durations are the frame times")
+    ap.add_argument("--pipelined", choices=["auto", "off"], default="auto",
+                    help="also time the same K frames with the other basis (2 frames in flight if --inflight "
+                         "is 1, else 1), reported beside `value` at every N (single_frame / pipelined); "
+                         "off for rocprof runs, whose kernel averages must be the single frame's")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -104,8 +107,6 @@ def parse():
         a.steps = 100 if a.workload == "c1" else 5
     if a.warmup is None:
         a.warmup = 5 if a.workload == "c1" else 1
-    if a.inflight is None:
-        a.inflight = 1 if a.gpus == 1 else 2
     return a
 
 
@@ -382,6 +383,34 @@ def first_process(wl, spp, depth, seed, n_dev):
     return d
 
 
+
+def rank_summary(per_rank, inflight, other_nf, steps, warmup):
+    """The cross-rank part of the line from every rank's own record: both
+    throughput bases at every N (single_frame: one frame at a time per rank;
+    pipelined: 2 frames in flight per rank), `scaling_basis` naming the one
+    `value` is (--inflight), and per rank its device (ordinal, UUID, PCI bus:
+    a SCALE line shows N distinct devices), rows and times."""
+    bases = {}
+    for nf, el_key, smp_key in ((inflight, "elapsed_s", "samples"), (other_nf, "other_elapsed_s", "other_samples")):
+        if nf is None:
+            continue
+        el = max(r[el_key] for r in per_rank)
+        sm = sum(r[smp_key] for r in per_rank)
+        bases["single_frame" if nf == 1 else "pipelined"] = {
+            "value": sm / el / 1e6, "unit": "Mray-samples/s", "ms_per_frame": el / steps * 1e3,
+            "streams_per_rank": nf, "steps": steps, "warmup": warmup * nf}
+    mpf = [r["ms_per_frame"] for r in per_rank]
+    per = {"rank": [r["rank"] for r in per_rank], "device": [r["device"] for r in per_rank],
+           "device_uuid": [r["device_uuid"] for r in per_rank], "pci_bus_id": [r["pci_bus_id"] for r in per_rank],
+           "distinct_devices": len({(r["device_uuid"], r["pci_bus_id"], r["device"]) for r in per_rank}),
+           "kernel_ms_avg": [r["kernel_ms_avg"] for r in per_rank], "rows": [r["rows"] for r in per_rank],
+           "ms_per_frame": mpf, "imbalance": max(mpf) / (sum(mpf) / len(mpf)),
+           "elapsed_ms": [r["elapsed_s"] * 1e3 for r in per_rank],
+           "elapsed_with_closing_barrier_ms": max(r["elapsed_barrier_s"] for r in per_rank) * 1e3}
+    return {"scaling_basis": "single_frame" if inflight == 1 else "pipelined",
+            "single_frame": bases.get("single_frame"), "pipelined": bases.get("pipelined"), "per_rank": per}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -434,25 +463,33 @@ def main():
     p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
     rows = check(lib.rt_rows_out(C.byref(p)))
     assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
-    # frames in flight: frame k on streams[k % inflight], each stream its own
+    # frames in flight: frame k on streams[k % nf], each stream its own
     # output buffer (and, in the library, its own tile-order record and split
     # sums); the frames are independent, so frame k+1's workgroups take the
-    # slots frame k's tail frees
+    # slots frame k's tail frees.  `value` is timed with
+    # --inflight frames in flight (1 by default, at every N: single-frame
+    # throughput); the other basis (2 if --inflight is 1) is timed the same
+    # way after it and reported beside it (single_frame / pipelined)
     inflight = max(1, a.inflight)
-    ps = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
-    if inflight > 1:
-        ps.flags |= RT_FLAG_STREAMED
-    streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
-    outs = [torch.empty(rows * W * 3, dtype=torch.float32, device=dev) for _ in range(inflight)]
+    other_nf = (2 if inflight == 1 else 1) if a.pipelined == "auto" else None
+    n_streams = max(inflight, other_nf or 1)
+    streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+    outs = [torch.empty(rows * W * 3, dtype=torch.float32, device=dev) for _ in range(n_streams)]
     out = outs[0]
     counters = torch.zeros(2, dtype=torch.int64, device=dev)
     stream = streams[0]
     sh = C.c_void_p(stream.cuda_stream)
     shs = [C.c_void_p(x.cuda_stream) for x in streams]
 
-    def step(k=0, params=ps):
-        check(lib.rt_launch(ds, C.byref(cam), C.byref(params), C.c_void_p(outs[k % inflight].data_ptr()),
-                            C.c_void_p(counters.data_ptr()), shs[k % inflight]))
+    def params_for(nf):
+        q = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
+        if nf > 1:
+            q.flags |= RT_FLAG_STREAMED
+        return q
+
+    def step(k=0, params=p, nf=1):
+        check(lib.rt_launch(ds, C.byref(cam), C.byref(params), C.c_void_p(outs[k % nf].data_ptr()),
+                            C.c_void_p(counters.data_ptr()), shs[k % nf]))
 
     def barrier():
         if world > 1:
@@ -498,34 +535,51 @@ def main():
         plain_ms = g0.elapsed_time(g1)
         check(lib.rt_set_schedule(a.schedule))
         step(0, p)   # (the record again, for the timed steps)
-    for k in range(a.warmup * inflight):
-        step(k)
-    torch.cuda.synchronize()
-    counters.zero_()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        s_k = streams[k % inflight]
-        starts[k].record(s_k)
-        step(k)
-        ends[k].record(s_k)
-    torch.cuda.synchronize()
-    # each rank's own steps, from the common barrier to its last kernel's end;
-    # the max over ranks below is the job's time (the closing barrier itself,
-    # a host round trip of every rank, is not render time: elapsed_barrier_s)
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    cnt = counters.to("cpu").tolist()
-    mine = {"rank": rank, "device": device, "elapsed_s": elapsed, "elapsed_barrier_s": time.perf_counter() - t0,
+
+    def timed(nf):
+        """W * nf warm-up frames, then exactly K frames bracketed by barrier +
+        synchronize; this rank's elapsed time, per-frame spans, counters."""
+        pq = params_for(nf)
+        for k in range(a.warmup * nf):
+            step(k, pq, nf)
+        torch.cuda.synchronize()
+        counters.zero_()
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            s_k = streams[k % nf]
+            starts[k].record(s_k)
+            step(k, pq, nf)
+            ends[k].record(s_k)
+        torch.cuda.synchronize()
+        # each rank's own steps, from the common barrier to its last kernel's
+        # end; the max over ranks is the job's time (the closing barrier itself,
+        # a host round trip of every rank, is not render time: elapsed_barrier_s)
+        t1 = time.perf_counter()
+        barrier()
+        spans = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+        cnt = counters.to("cpu").tolist()
+        return {"elapsed_s": t1 - t0, "elapsed_barrier_s": time.perf_counter() - t0, "spans": spans,
+                "segments": cnt[0], "samples": cnt[1]}
+
+    main_t = timed(inflight)
+    other_t = timed(other_nf) if other_nf else None
+    kern_ms = main_t["spans"]
+    props = torch.cuda.get_device_properties(dev)
+    mine = {"rank": rank, "device": device, "device_name": props.name,
+            "device_uuid": str(getattr(props, "uuid", "")), "pci_bus_id": getattr(props, "pci_bus_id", None),
+            "local_rank": local, "visible_devices": ndev,
+            "elapsed_s": main_t["elapsed_s"], "elapsed_barrier_s": main_t["elapsed_barrier_s"],
             "kernel_ms_avg": single_ms if single_ms is not None else sum(kern_ms) / len(kern_ms),
             "launch_span_ms_avg": sum(kern_ms) / len(kern_ms),
-            "kernel_ms_max": max(kern_ms), "rows": rows, "segments": cnt[0], "samples": cnt[1],
-            "first_launch_ms": first_ms, "plain_ms": plain_ms, "ms_per_frame": elapsed / a.steps * 1e3}
+            "kernel_ms_max": max(kern_ms), "rows": rows, "segments": main_t["segments"],
+            "samples": main_t["samples"], "first_launch_ms": first_ms, "plain_ms": plain_ms,
+            "ms_per_frame": main_t["elapsed_s"] / a.steps * 1e3,
+            "other_elapsed_s": other_t["elapsed_s"] if other_t else None,
+            "other_samples": other_t["samples"] if other_t else None}
     per_rank = [mine]
     if world > 1:
         per_rank = [None] * world
@@ -534,6 +588,7 @@ def main():
     segs_total = sum(r["segments"] for r in per_rank)
     samples_total = sum(r["samples"] for r in per_rank)
     kern_avg_ms = mine["kernel_ms_avg"]
+    summary = rank_summary(per_rank, inflight, other_nf, a.steps, a.warmup)
 
     res = None
     if rank == 0:
@@ -603,6 +658,8 @@ def main():
                                        "after a launch of another shape; plain_schedule_off_ms: the same frame with "
                                        "the schedule off (rt_set_schedule(1)); the timed steps dispatch longest first by "
                                        "the previous launches' per-tile durations (each added to half the record before it)"},
+            "scaling_basis": summary["scaling_basis"], "single_frame": summary["single_frame"],
+            "pipelined": summary["pipelined"],
             "frames_in_flight": {"streams": inflight, "rt_launch_flags": "RT_FLAG_STREAMED" if inflight > 1 else 0,
                                  "launch_span_ms_avg": mine["launch_span_ms_avg"],
                                  "note": "timed frames go round-robin to this many streams (independent frames: "
@@ -610,12 +667,7 @@ def main():
                                          "kernel_ms_avg and the roofline are the same frame launched alone on one "
                                          "stream; launch_span_ms_avg = each timed frame's start-to-end on its stream "
                                          "(spans overlap)"},
-            "per_rank": {"kernel_ms_avg": kms, "rows": [r["rows"] for r in per_rank],
-                         "ms_per_frame": [r["ms_per_frame"] for r in per_rank],
-                         "imbalance": max(r["ms_per_frame"] for r in per_rank) /
-                                      (sum(r["ms_per_frame"] for r in per_rank) / len(per_rank)),
-                         "elapsed_ms": [r["elapsed_s"] * 1e3 for r in per_rank],
-                         "elapsed_with_closing_barrier_ms": max(r["elapsed_barrier_s"] for r in per_rank) * 1e3},
+            "per_rank": summary["per_rank"],
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_total / a.steps,
             "kernel": "rtclj::trace_kernel<SRC,SCAN,STATS> (default: BVH with 4-body leaves in LDS, 8x8-pixel "
                       "sample pool per 256-thread workgroup, fixed-point colour sums in LDS)",

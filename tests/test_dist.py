@@ -106,3 +106,48 @@ def test_bench_defaults_to_row_tile_strong_scaling(monkeypatch):
     p1 = shard_params(2, 1, 1200, 675, 100, 50, scaling=a.scaling)
     assert (p0["tile_first"], p1["tile_first"], p0["tile_step"]) == (0, 1, 2)
     assert set(bench.WORKLOADS) == {"c1", "c2", "c3", "c4"}
+    # value is single-frame throughput at every N: the same
+    # basis at N = 1 and N > 1, the pipelined one timed beside it
+    assert a.inflight == 1 and b.inflight == 1 and a.pipelined == "auto"
+
+
+def _summary_worker(rank, world, port, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "raytracing-clj_amd")]
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rank's own record as bench.main() builds it (times of a made-up frame)
+    mine = {"rank": rank, "device": rank, "device_uuid": f"GPU-{rank:02d}", "pci_bus_id": 0x10 + rank,
+            "elapsed_s": 1.0 + rank, "elapsed_barrier_s": 1.1 + rank, "kernel_ms_avg": 10.0, "rows": 80 + rank,
+            "samples": 1000, "ms_per_frame": 10.0 * (1 + rank), "other_elapsed_s": 0.5, "other_samples": 1000}
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, mine)
+    if rank == 0:
+        q.put(bench.rank_summary(per_rank, 1, 2, 100, 5))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_line_names_its_basis_and_devices():
+    """The cross-rank part of bench.py's line, from records gathered over a
+    world-size-2 gloo job: both bases (single_frame, pipelined) with value =
+    samples of all ranks / the slowest rank's time, scaling_basis naming the
+    one `value` is, and each rank's device ordinal / UUID / PCI bus."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_summary_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    s = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert s["scaling_basis"] == "single_frame"
+    assert s["single_frame"]["value"] == pytest.approx(2000 / 2.0 / 1e6)   # max elapsed over ranks
+    assert s["pipelined"]["value"] == pytest.approx(2000 / 0.5 / 1e6) and s["pipelined"]["streams_per_rank"] == 2
+    pr = s["per_rank"]
+    assert pr["device"] == [0, 1] and pr["device_uuid"] == ["GPU-00", "GPU-01"] and pr["distinct_devices"] == 2
+    assert pr["rows"] == [80, 81] and pr["imbalance"] == pytest.approx(20 / 15)
