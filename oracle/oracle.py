@@ -35,6 +35,10 @@ def _lib():
         d.oracle_render.restype = C.c_int
         d.oracle_render.argtypes = [C.c_int, C.c_int, dp, ip, dp, dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, fp, dp, u64p]
+        d.oracle_render_cols.restype = C.c_int
+        d.oracle_render_cols.argtypes = [C.c_int, C.c_int, dp, ip, dp, dp, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                         C.c_int, fp, dp, u64p]
         d.oracle_sphere_hit.restype = C.c_int
         d.oracle_sphere_hit.argtypes = [dp, dp, dp, C.c_double, C.c_double, dp]
         d.oracle_reflect.argtypes = [dp, dp, dp]
@@ -60,23 +64,25 @@ def _d(a):
 
 
 def render(mode, sphere, kind, mat, cam, defocus, width, height, spp, max_depth, seed=1, rows=None,
-           sample_begin=0, nthreads=0, want64=False, row_step=1):
+           sample_begin=0, nthreads=0, want64=False, row_step=1, cols=None):
     """Render rows r0, r0+row_step, ... < r1 (default all) -> (float32 (rows,W,3),
-    float64 or None, segments, samples)."""
+    float64 or None, segments, samples).  cols=(c0, c1): only those columns
+    of the rows (the others NaN; samples counts the rendered pixels')."""
     r0, r1 = (0, height) if rows is None else rows
     nrows = (r1 - r0 + row_step - 1) // row_step
     sph, sp = _d(np.asarray(sphere, np.float64).reshape(-1, 4))
     mt, mp = _d(np.asarray(mat, np.float64).reshape(-1, 4))
     kd = np.ascontiguousarray(kind, np.int32).reshape(-1)
     cm, cp = _d(np.asarray(cam, np.float64).reshape(18))
-    out = np.empty((nrows, width, 3), np.float32)
-    out64 = np.empty((nrows, width, 3), np.float64) if want64 else None
+    c0, c1 = (0, width) if cols is None else cols
+    out = np.full((nrows, width, 3), np.nan, np.float32)
+    out64 = np.full((nrows, width, 3), np.nan, np.float64) if want64 else None
     cnt = np.zeros(2, np.uint64)
-    rc = _lib().oracle_render(mode, len(kd), sp, kd.ctypes.data_as(C.POINTER(C.c_int)), mp, cp, int(defocus),
-                              width, height, r0, r1, row_step, spp, sample_begin, max_depth, seed, nthreads,
-                              out.ctypes.data_as(C.POINTER(C.c_float)),
-                              out64.ctypes.data_as(C.POINTER(C.c_double)) if want64 else None,
-                              cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
+    rc = _lib().oracle_render_cols(mode, len(kd), sp, kd.ctypes.data_as(C.POINTER(C.c_int)), mp, cp, int(defocus),
+                                   width, height, r0, r1, row_step, c0, c1, spp, sample_begin, max_depth, seed,
+                                   nthreads, out.ctypes.data_as(C.POINTER(C.c_float)),
+                                   out64.ctypes.data_as(C.POINTER(C.c_double)) if want64 else None,
+                                   cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
     if rc != 0:
         raise ValueError(f"oracle_render rejected its arguments (rc={rc})")
     return out, out64, int(cnt[0]), int(cnt[1])

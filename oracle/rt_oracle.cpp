@@ -562,12 +562,14 @@ extern "C" {
 // optionally out64 in double for MODE_REF64).  sphere/mat: n x 4 doubles,
 // cam: 18 doubles (center, p00, du, dv, disk_u, disk_v).  nthreads <= 0 ->
 // hardware concurrency.  counters (nullable): [segments, samples].
-int oracle_render(int mode, int n, const double* sphere, const int* kind, const double* mat,
-                  const double* cam, int defocus, int width, int height, int row_begin, int row_end,
-                  int row_step, int spp, int sample_begin, int max_depth, uint64_t seed, int nthreads,
-                  float* out, double* out64, uint64_t* counters) {
+// oracle_render_cols: only columns [col_begin, col_end) of those rows (the
+// others are left as they are in out); oracle_render: every column.
+int oracle_render_cols(int mode, int n, const double* sphere, const int* kind, const double* mat,
+                       const double* cam, int defocus, int width, int height, int row_begin, int row_end,
+                       int row_step, int col_begin, int col_end, int spp, int sample_begin, int max_depth,
+                       uint64_t seed, int nthreads, float* out, double* out64, uint64_t* counters) {
   if (width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_end < row_begin || !out ||
-      row_step <= 0 ||
+      row_step <= 0 || col_begin < 0 || col_end > width || col_end < col_begin ||
       (n > 0 && (!sphere || !kind || !mat)) || !cam || mode < MODE_REF64 || mode > MODE_REALM32)
     return -1;
   Job J{};
@@ -606,14 +608,17 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
   if (spp <= 0 || max_depth <= 0) {
     // depth <= 0 -> black (raytracing.clj:46-47); spp 0 -> 0/0 in the
     // reference, defined here (and on the GPU) as 0/1 = black.
-    std::fill(out, out + static_cast<size_t>(rows) * width * 3, 0.0f);
-    if (out64) std::fill(out64, out64 + static_cast<size_t>(rows) * width * 3, 0.0);
+    for (int r = 0; r < rows; ++r) {
+      const size_t o = (static_cast<size_t>(r) * width + col_begin) * 3, m = static_cast<size_t>(col_end - col_begin) * 3;
+      std::fill(out + o, out + o + m, 0.0f);
+      if (out64) std::fill(out64 + o, out64 + o + m, 0.0);
+    }
     if (counters) counters[0] = counters[1] = 0;
     return 0;
   }
   // work items: 32-pixel row chunks, handed out by an atomic counter
   constexpr int CH = 32;
-  const int per_row = (width + CH - 1) / CH;
+  const int per_row = (col_end - col_begin + CH - 1) / CH;
   const int items = rows * per_row;
   int nt = nthreads > 0 ? nthreads : static_cast<int>(std::thread::hardware_concurrency());
   nt = std::max(1, std::min(nt, std::max(items, 1)));
@@ -621,8 +626,8 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
   std::vector<uint64_t> segs(nt, 0);
   auto work = [&](int tid) {
     for (int it; (it = next.fetch_add(1)) < items;) {
-      const int r = it / per_row, x0 = (it % per_row) * CH;
-      render_row(J, r, x0, std::min(width, x0 + CH), &segs[tid]);
+      const int r = it / per_row, x0 = col_begin + (it % per_row) * CH;
+      render_row(J, r, x0, std::min(col_end, x0 + CH), &segs[tid]);
     }
   };
   if (nt == 1) {
@@ -636,9 +641,17 @@ int oracle_render(int mode, int n, const double* sphere, const int* kind, const 
     uint64_t s = 0;
     for (auto v : segs) s += v;
     counters[0] = s;
-    counters[1] = static_cast<uint64_t>(rows) * width * spp;
+    counters[1] = static_cast<uint64_t>(rows) * (col_end - col_begin) * spp;
   }
   return 0;
+}
+
+int oracle_render(int mode, int n, const double* sphere, const int* kind, const double* mat,
+                  const double* cam, int defocus, int width, int height, int row_begin, int row_end,
+                  int row_step, int spp, int sample_begin, int max_depth, uint64_t seed, int nthreads,
+                  float* out, double* out64, uint64_t* counters) {
+  return oracle_render_cols(mode, n, sphere, kind, mat, cam, defocus, width, height, row_begin, row_end, row_step,
+                            0, width, spp, sample_begin, max_depth, seed, nthreads, out, out64, counters);
 }
 
 // ---- known-answer entry points (fp64 reference formulas) ----

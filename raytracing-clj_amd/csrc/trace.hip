@@ -121,6 +121,7 @@ struct alignas(16) KArgs {
   unsigned long long* stealc;    // [helpers that got samples, samples they claimed] (rt_steal_stats)
   int n_owner;
   int n_units;
+  int share_from;                // units before this one never share (they end long before the launch's tail)
   int steal_min;
   int batch_max;                 // a wave's largest claim on a shared tile (0: by the pool)
   unsigned epoch;                // this launch's (per stream, 1 .. 65535)
@@ -510,7 +511,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // order is needed between the two: a helper that reads the word before it
   // lands sees another epoch and leaves it alone.  done[tile] is 0 already:
   // zeroed at allocation and by the workgroup that completes a shared tile.)
-  const bool shared_tile = !kRing && ka->word && !split && (!own || pool > 512);
+  // Only the units dispatched in the launch's last rounds (unit >= share_from)
+  // publish: an earlier unit ends while later ones still start, so no helper
+  // would ever join it, and its claims would all be HBM atomics (C4: ~60 per
+  // tile, 3 GB of WRITE_SIZE per launch when every unit published).
+  const bool shared_tile = !kRing && ka->word && !split && (!own || (pool > 512 && unit >= ka->share_from));
   // where the waves claim their batches: the shared tile's word, else (NULL)
   // the workgroup's s_pool_next
   unsigned long long* const src = shared_tile ? ka->word + tile : nullptr;
@@ -2506,6 +2511,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMemsetAsync(sch->owner, 0xff, n_owner * sizeof(int), stream));
       HIP_TRY(hipMemsetAsync(sch->word, 0, n_tiles * sizeof(unsigned long long), stream));
     }
+    // owners publish only in the launch's last RTCLJ_SHARE_ROUNDS rounds of
+    // units (default 2; a round = the workgroups the device holds at once)
+    a.share_from = static_cast<int>(std::max<int64_t>(
+        0, n_units - static_cast<int64_t>(env_int("RTCLJ_SHARE_ROUNDS", 2, 0)) * slots));
     a.word = sch->word;
     a.done = sch->done;
     a.sum = sch->sum;

@@ -6,14 +6,14 @@ fp64 reference-semantics pin of the benchmark workload.
      full spp, with tests/test_oracle_cover_pin.py's tolerances, and the
      segments per sample within 2e-3 of REF64's;
   C2 3840x2160, 500 spp (484 bodies): the whole frame, deterministic,
-     finite, in range, six rows spread over the frame bit-exact against the
-     fp32 mirror at full spp;
+     finite, in range, six rows spread over the frame and two through the
+     r = 1 glass body bit-exact against the fp32 mirror at full spp;
   C3 3840x2160, 1000 spp, row tiles over 8 GPUs + host gather: rt_render's
      8-way fan-out (RT_FLAG_SHARDS_ON_DEVICE0 puts the 8 shards on this box's
      one GPU) bit-identical to the 1-shard frame;
   C4 7680x4320, 2000 spp, depth 64, 1000 bodies: the whole frame's
      properties, a row band re-rendered alone equal to the frame's rows, and
-     a 64-pixel strip bit-exact against the mirror at full spp; and C4's own
+     eight 64-pixel strips bit-exact against the mirror at full spp; and C4's own
      kernel (8-body leaves, u8 stack, 8x4 tiles) on every 270th row against
      MODE_REF64 at 16 spp (the cover pin's bounds, as for C1).
 
@@ -43,10 +43,10 @@ NT = min(16, os.cpu_count() or 1)   # the GPU box's CPU share
 SEGS = json.loads((Path(__file__).resolve().parent / "golden" / "segs_ref64.json").read_text())["configs"]
 
 
-def _oracle(mode, sc, cam, w, h, spp, depth, rows=None, row_step=1):
+def _oracle(mode, sc, cam, w, h, spp, depth, rows=None, row_step=1, cols=None):
     out, _, segs, smp = oracle.render(mode, sc.sphere.astype(np.float64), sc.kind, sc.mat.astype(np.float64),
                                       cam.as_list(), cam.defocus, w, h, spp, depth, seed=1, rows=rows,
-                                      row_step=row_step, nthreads=NT)
+                                      row_step=row_step, nthreads=NT, cols=cols)
     return out, segs, smp
 
 
@@ -119,6 +119,13 @@ def test_c2_full_frame(gpu_lib):
     ref, segs, smp = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, 50, rows=(180, h), row_step=360)
     assert ref.shape[0] == 6
     bad = [r for k, r in enumerate(range(180, h, 360)) if not np.array_equal(a[r], ref[k])]
+    # and two rows through the r = 1 glass body at (0, 1, 0) (it spans rows
+    # ~161-1080 around column 1920; row 626 is its centre): refraction, total
+    # internal reflection and Schlick draws over a wide run of pixels
+    for r in (400, 626):
+        g, _, _ = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, 50, rows=(r, r + 1))
+        if not np.array_equal(a[r], g[0]):
+            bad.append(r)
     assert not bad, bad
 
 
@@ -153,10 +160,17 @@ def test_c4_full_frame(gpu_lib):
     # a band rendered alone (row_begin offset, other tiling) == the frame's rows
     band = R.render(sc, cam, w, h, spp=spp, max_depth=depth, seed=1, rows=(2100, 2116))
     assert np.array_equal(band, img[2100:2116])
-    # a 64-pixel strip of one row, full spp, against the fp32 mirror
-    r = 2500
-    ref, _, _ = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, depth, rows=(r, r + 1))
-    assert np.array_equal(img[r, 3000:3064], ref[0, 3000:3064])
+    # eight 64-pixel strips spread over the frame, full spp, against the fp32
+    # mirror: the r = 1 glass (centre row 1252, column 3840), lambertian
+    # (1043, 3199) and metal (1629, 5001) bodies, sky, the field, the near
+    # ground and the frame's last row and columns
+    bad = []
+    for r, c0 in ((1252, 3808), (1043, 3168), (1629, 4970), (200, 6000), (2600, 2500), (2200, 5800),
+                  (3800, 1000), (4319, 7616)):
+        ref, _, _ = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, depth, rows=(r, r + 1), cols=(c0, c0 + 64))
+        if not np.array_equal(img[r, c0:c0 + 64], ref[0, c0:c0 + 64]):
+            bad.append((r, c0))
+    assert not bad, bad
 
 
 def test_c4_against_fp64_reference_semantics(gpu_lib):
