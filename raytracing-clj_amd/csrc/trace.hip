@@ -246,6 +246,13 @@ __device__ __forceinline__ unsigned long long xread64(unsigned long long* p) {
 __device__ __forceinline__ int xread32(int* p) {
   return __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A helper's look at the owner table and tile words only guides its choice
+// (its join is an RMW on the word, whose returned value decides): relaxed
+// agent-scope loads (global_load sc1), a read with no write-back, suffice.
+__device__ __forceinline__ unsigned long long xload64(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int xload32(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ bool xcas64(unsigned long long* p, unsigned long long& expect, unsigned long long v) {
   return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
@@ -346,6 +353,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   __shared__ int s_join;              // helpers the owner's claims saw (> 0: the tile was shared)
   __shared__ int s_unit[2];           // a helper's tile and first index
   __shared__ unsigned long long s_best;
+  __shared__ unsigned long long s_segs;   // the workgroup's segments (counters)
   __shared__ int s_last;
   // drain compaction: per wave the paths it posted and how many were taken;
   // the waves still in the hot loop
@@ -406,9 +414,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       int w = w0 + static_cast<int>(threadIdx.x) + 256 * i;
       w = w >= M ? w - M : w;
       w = w >= M ? w % M : w;
-      const int t = xread32(&ka->owner[w]);
+      const int t = xload32(&ka->owner[w]);
       if (t >= 0) {
-        const unsigned long long wd = xread64(&ka->word[t]);
+        const unsigned long long wd = xload64(&ka->word[t]);
         const int fr = word_epoch(wd) == ka->epoch ? tile_pool(ka, t) - static_cast<int>(static_cast<unsigned>(wd)) : 0;
         const unsigned long long k2 = (static_cast<unsigned long long>(fr) << 32) | static_cast<unsigned>(t);
         key = (fr >= ka->steal_min && k2 > key) ? k2 : key;
@@ -529,6 +537,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       s_cnt = 256;
     }
     s_join = own ? 0 : 1;
+    s_segs = 0ull;
     s_pool_next = kRing ? 0 : 256;   // (the ring claims its own)
     s_alive = 4;
     s_mb_avail = 0;   // (posted, not yet taken: a hint for the waves' exits to the step)
@@ -1678,11 +1687,14 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     }
   }
   if (a.counters) {
-    // one 64-bit atomic per wave: the segments of its 64 lanes; the samples
-    // once per workgroup
+    // the workgroup's segments (its waves' sums met in LDS) in one 64-bit
+    // atomic, beside its samples (one per workgroup each: a global atomic is
+    // an HBM read-modify-write)
     uint32_t v = segs;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0 && v) atomicAdd(&a.counters[0], static_cast<unsigned long long>(v));
+    if (lane == 0 && v) atomicAdd(&s_segs, static_cast<unsigned long long>(v));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_segs) atomicAdd(&a.counters[0], s_segs);
   }
 }
 
@@ -2512,9 +2524,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMemsetAsync(sch->word, 0, n_tiles * sizeof(unsigned long long), stream));
     }
     // owners publish only in the launch's last RTCLJ_SHARE_ROUNDS rounds of
-    // units (default 2; a round = the workgroups the device holds at once)
+    // units (default 3; a round = the workgroups the device holds at once.
+    // C4: WRITE_SIZE 2.90 -> 0.44 GB per launch at 2, C1's timing the same
+    // at 1, 2, 3 or every round: profiles/r04/share_rounds/)
     a.share_from = static_cast<int>(std::max<int64_t>(
-        0, n_units - static_cast<int64_t>(env_int("RTCLJ_SHARE_ROUNDS", 2, 0)) * slots));
+        0, n_units - static_cast<int64_t>(env_int("RTCLJ_SHARE_ROUNDS", 3, 0)) * slots));
     a.word = sch->word;
     a.done = sch->done;
     a.sum = sch->sum;

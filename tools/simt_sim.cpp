@@ -38,6 +38,8 @@ static double g_cand = 0, g_rej = 0, g_segs = 0, g_visits = 0, g_leafs = 0;
 static float g_pad = 1.0f;
 static int g_big_leaves = 0;
 static int g_tile_h = 8;      // workgroup pool: 8 x g_tile_h pixels (TILEH)
+static int g_nw = 4;          // waves per workgroup (NW; 8 with TILEH=16: 512 threads)
+static double C_XCHG = 0;     // per wave-iteration cost of the sort policies' LDS path exchange (XCHG)
 static int g_exact_mode = 0;   // 0: one pass per candidate of the busiest lane; 1: one block per leaf body
 static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
 static double g_abs = 0;   // wave iterations with a metal absorption
@@ -373,9 +375,10 @@ struct Result { double cost = 0, iters = 0, steps = 0, samples = 0, lane_steps =
 // one workgroup tile (8x8 pixels at (tx, ty)) under a policy
 static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Result& R) {
   const int npx = 64 * g_tile_h / 8, pool = npx * C.spp;   // 8 x g_tile_h pixels
-  std::vector<Path> lanes(256);
+  const int NL = 64 * g_nw;
+  std::vector<Path> lanes(NL);
   int next = 0;
-  for (int l = 0; l < 256; ++l) lanes[l].j = next < pool ? next++ : -1;
+  for (int l = 0; l < NL; ++l) lanes[l].j = next < pool ? next++ : -1;
   auto pixel = [&](int j, int& px, int& py) {
     const int q = j / C.spp;
     px = tx * 8 + q % 8;
@@ -388,7 +391,7 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
     // those lanes and sets up their next segment (camera ray if the path
     // ended); the others keep their traversal state across the phase
     struct L { Trav t; size_t i = 0; bool ended = false, live = false; };
-    std::vector<L> st(256);
+    std::vector<L> st(NL);
     auto setup = [&](int l) {   // trace lane l's next segment (shading applied at its end)
       Path& p = lanes[l];
       st[l] = L{};
@@ -398,9 +401,9 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
       st[l].ended = step(C, p, px, py, st[l].t);
       st[l].live = true;
     };
-    for (int l = 0; l < 256; ++l) setup(l);
-    double wc[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 4; ++k) {   // first phase: the camera rays' set-up
+    for (int l = 0; l < NL; ++l) setup(l);
+    std::vector<double> wc(g_nw, 0.0);
+    for (int k = 0; k < g_nw; ++k) {   // first phase: the camera rays' set-up
       int md = 0, mb = 0, ob = 0;
       for (int l = 64 * k; l < 64 * k + 64; ++l)
         if (st[l].live) {
@@ -412,7 +415,7 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
     }
     for (;;) {
       int w = -1;
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < g_nw; ++k) {
         bool any = false;
         for (int l = 0; l < 64; ++l) any |= st[64 * k + l].live;
         if (any && (w < 0 || wc[k] < wc[w])) w = k;
@@ -473,10 +476,10 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
   }
   if (policy == 0) {
     // 4 independent waves, advanced in order of accumulated cost
-    double wc[4] = {0, 0, 0, 0};
+    std::vector<double> wc(g_nw, 0.0);
     for (;;) {
       int w = -1;
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < g_nw; ++k) {
         bool any = false;
         for (int l = 0; l < 64; ++l) any |= lanes[64 * k + l].j >= 0;
         if (any && (w < 0 || wc[k] < wc[w])) w = k;
@@ -535,10 +538,10 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
     // all 256 lanes step together; paths dealt to waves sorted by key
     for (;;) {
       std::vector<int> live;
-      for (int l = 0; l < 256; ++l)
+      for (int l = 0; l < NL; ++l)
         if (lanes[l].j >= 0) live.push_back(l);
       if (live.empty()) break;
-      std::vector<int> oracle_len(256, 0);
+      std::vector<int> oracle_len(NL, 0);
       if (key_mode == 3)   // upper bound: the segment's own visit count (traced on a copy)
         for (int l : live) {
           Path cp = lanes[l];
@@ -558,7 +561,7 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
         return 1 + oct;
       };
       std::stable_sort(live.begin(), live.end(), [&](int a, int b) { return key(lanes[a]) < key(lanes[b]); });
-      std::vector<Trav> tr(256);
+      std::vector<Trav> tr(NL);
       std::vector<int> done;
       for (size_t w = 0; w * 64 < live.size(); ++w) {
         std::vector<const Trav*> act;
@@ -571,7 +574,7 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
           act.push_back(&tr[l]);
           R.lane_steps += tr[l].leaves.size();
         }
-        R.cost += wave_cost(act, &R.steps) + C_SORT;
+        R.cost += wave_cost(act, &R.steps) + C_SORT + C_XCHG;
         R.iters += 1;
       }
       for (int l : done) {
@@ -664,6 +667,9 @@ int main(int argc, char** argv) {
   const double lf[3] = {13, 2, 3}, la[3] = {0, 0, 0}, vup[3] = {0, 1, 0};
   rt_camera_setup(1200, 675, 20.0, lf, la, vup, 0.6, 10.0, &C.cam);
   if (std::getenv("TILEH")) g_tile_h = std::atoi(std::getenv("TILEH"));
+  if (std::getenv("NW")) g_nw = std::atoi(std::getenv("NW"));
+  if (std::getenv("XCHG")) C_XCHG = std::atof(std::getenv("XCHG"));
+  if (std::getenv("CSORT")) C_SORT = std::atof(std::getenv("CSORT"));
   const int gx = 1200 / 8, gy = (675 + g_tile_h - 1) / g_tile_h;
   std::vector<int> pick;
   uint32_t h = 12345;
