@@ -2465,7 +2465,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // the grid: the units, then (stealing) the thieves, dispatched last, i.e.
   // as the units' slots free up in the launch's tail
   int64_t grid = n_units;
-  if (steal && split == 1) {
+  // Sharing balances a launch whose tiles have no cost record (plain order:
+  // a process's or a shape's first frame).  In the recorded longest-first
+  // order the cheap tiles come last and the tail is short without it (C1
+  // 5.94 ms either way), while its claims and helpers' scans are HBM atomics
+  // (C1: 31 vs 11 MB per launch; profiles/r04/share_rounds/): off there
+  // unless RTCLJ_SHARE_RECORDED=1.
+  if (steal && split == 1 && (!a.tile_order || env_int("RTCLJ_SHARE_RECORDED", 0, 0) != 0)) {
     const int slots = std::max(1, launch_slots(ds->device, v.fn, lds));
     const int n_owner = 2 * slots;   // owner entries: twice the resident workgroups
     // (at most 32 per slot: a tile's helper count stays below 2^16)
@@ -2524,11 +2530,12 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMemsetAsync(sch->word, 0, n_tiles * sizeof(unsigned long long), stream));
     }
     // owners publish only in the launch's last RTCLJ_SHARE_ROUNDS rounds of
-    // units (default 3; a round = the workgroups the device holds at once.
-    // C4: WRITE_SIZE 2.90 -> 0.44 GB per launch at 2, C1's timing the same
-    // at 1, 2, 3 or every round: profiles/r04/share_rounds/)
+    // units (default 2; a round = the workgroups the device holds at once.
+    // C4 plain order: WRITE_SIZE 2.90 GB per launch at every round, 0.44 at
+    // 2, 0.60 at 3; C1's timing the same at 1, 2, 3 or every round:
+    // profiles/r04/share_rounds/)
     a.share_from = static_cast<int>(std::max<int64_t>(
-        0, n_units - static_cast<int64_t>(env_int("RTCLJ_SHARE_ROUNDS", 3, 0)) * slots));
+        0, n_units - static_cast<int64_t>(env_int("RTCLJ_SHARE_ROUNDS", 2, 0)) * slots));
     a.word = sch->word;
     a.done = sch->done;
     a.sum = sch->sum;

@@ -50,7 +50,7 @@ def cover(gpu_lib):
 
 @pytest.mark.parametrize("knobs", [dict(RTCLJ_COMPACT="64"), dict(RTCLJ_COMPACT="16"), dict(RTCLJ_COMPACT="1"),
                                    dict(RTCLJ_COMPACT="5", RTCLJ_SPLIT="1"),
-                                   dict(RTCLJ_COMPACT="16", RTCLJ_SPLIT="1", RTCLJ_STEAL_MIN="1"),
+                                   dict(RTCLJ_COMPACT="16", RTCLJ_SPLIT="1", RTCLJ_STEAL_MIN="1", RTCLJ_SHARE_RECORDED="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_STEAL="0"),
                                    dict(RTCLJ_COMPACT="0")])
 def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):

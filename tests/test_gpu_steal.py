@@ -31,8 +31,11 @@ def _shard_rows(h, tile, first, step):
 @pytest.fixture(autouse=True)
 def share_always(monkeypatch):
     """These frames have few tiles: rt_launch would split their samples
-    instead of sharing them (RTCLJ_SPLIT=1 keeps every tile whole)."""
+    instead of sharing them (RTCLJ_SPLIT=1 keeps every tile whole); and a
+    launch in the recorded tile order shares only with
+    RTCLJ_SHARE_RECORDED=1 (by default only plain-order launches do)."""
     monkeypatch.setenv("RTCLJ_SPLIT", "1")
+    monkeypatch.setenv("RTCLJ_SHARE_RECORDED", "1")
 
 
 @pytest.fixture(scope="module")
@@ -78,6 +81,28 @@ def test_default_steals_on_a_frame_of_few_tiles(env):
         got, st = _launch(env, cam, p, s)
         assert np.array_equal(got, want), k
         assert st[0] > 0 and 0 < st[1] < w * h * spp, (k, st)
+
+
+def test_recorded_order_does_not_share_by_default(env, monkeypatch):
+    """By default only a launch without a tile-cost record (plain order)
+    shares its tiles: the first launch of a shape has helpers joining, the
+    next ones (recorded longest-first order) none -- every frame equal to
+    the mirror."""
+    from rtclj import scenes
+    from rtclj._lib import rt_params
+    sc, ds, torch = env
+    monkeypatch.delenv("RTCLJ_SHARE_RECORDED")
+    w, h, spp, seed = 24, 16, 600, 6
+    cam = scenes.cover_camera(w, h)
+    want = _mirror(sc, cam, w, h, spp, seed)
+    s = torch.cuda.Stream()
+    p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=50, seed=seed)
+    steals = []
+    for k in range(3):
+        got, st = _launch(env, cam, p, s)
+        assert np.array_equal(got, want), k
+        steals.append(st[0])
+    assert steals[0] > 0 and steals[1] == steals[2] == 0, steals
 
 
 @pytest.mark.parametrize("knobs", [dict(RTCLJ_STEAL_MIN="1"), dict(RTCLJ_STEAL_MIN="100000"),
