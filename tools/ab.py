@@ -20,6 +20,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "raytracing-clj_amd"))
 
 import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (before the library: torch's HIP runtime must serve the process)
 
 from rtclj import raytracing as R, scenes  # noqa: E402
 from rtclj._lib import check, diag_lib  # noqa: E402

@@ -3,8 +3,8 @@
 on one GPU: per setting and round, a shape change (so the frame's next
 launch has no tile-cost record: plain order, as a process's first frame),
 the first launch timed, then `--warm` launches and `--reps` timed launches in
-the recorded order.  Settings alternate within each round; every frame must
-be bit-identical to the first setting's.
+the recorded order.  Settings alternate within each round, in an order that
+rotates from round to round; every frame must be bit-identical.
 
   python tools/env_ab.py --set RTCLJ_SHARE_ROUNDS=2 --set RTCLJ_SHARE_ROUNDS=1000000 \
       [--workload c1] [--rounds 3] [--reps 10] [--json out.jsonl]
@@ -72,7 +72,9 @@ def main():
         return e0.elapsed_time(e1)
 
     for rnd in range(a.rounds):
-        for k in a.sets:
+        # the settings rotate: each round starts with the next one (the first
+        # launch after another setting's steady launches measured slower)
+        for k in a.sets[rnd % len(a.sets):] + a.sets[:rnd % len(a.sets)]:
             os.environ.clear()
             os.environ.update(base_env)
             os.environ.update(parse_setting(k))
@@ -85,7 +87,7 @@ def main():
             img = out.cpu()
             if ref is None:
                 ref = img
-            assert torch.equal(img, ref), f"setting {k}: frame differs from {a.sets[0]}"
+            assert torch.equal(img, ref), f"setting {k}: frame differs from the first one run"
             print(json.dumps({"round": rnd, "set": k, "first_ms": res[k]["first"][-1],
                               "steady_med_ms": statistics.median(res[k]["steady"][-a.reps:])}), flush=True)
     os.environ.clear()

@@ -26,7 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--variant", type=int, default=0)
     a = ap.parse_args()
+    check(lib.rt_set_variant(a.variant))
     wl = WORKLOADS[a.workload]
     w = wl["width"]
     h = R.image_height(w)

@@ -17,7 +17,8 @@ def main():
     per = defaultdict(dict)   # counter -> {dispatch: value}
     for f in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
-            if "trace_kernel" not in r["Kernel_Name"] or "true>" in r["Kernel_Name"]:
+            kn = r["Kernel_Name"]
+            if not ("trace_kernel" in kn or "sorted_kernel" in kn) or ("trace_kernel" in kn and "true>" in kn):
                 continue
             d = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)
             c = r["Counter_Name"]
@@ -27,6 +28,12 @@ def main():
         res["hbm_bytes_last"] = (2.0 * res["FETCH_SIZE"][-1] + res["WRITE_SIZE"][-1]) * 1024.0
         res["write_bytes_last"] = res["WRITE_SIZE"][-1] * 1024.0
         res["fetch_bytes_x2_last"] = res["FETCH_SIZE"][-1] * 2048.0
+    if "SQ_INSTS_VALU" in res and "SQ_THREAD_CYCLES_VALU" in res:
+        res["lanes_active_last"] = res["SQ_THREAD_CYCLES_VALU"][-1] / res["SQ_INSTS_VALU"][-1] / 64.0
+    if "SQ_ACTIVE_INST_VALU" in res and "GRBM_GUI_ACTIVE" in res:
+        res["issue_busy_last"] = res["SQ_ACTIVE_INST_VALU"][-1] * 4.0 / 1024 / (res["GRBM_GUI_ACTIVE"][-1] / 8)
+    if "SQ_WAVE_CYCLES" in res and "GRBM_GUI_ACTIVE" in res:
+        res["waves_per_simd_last"] = res["SQ_WAVE_CYCLES"][-1] * 4.0 / 1024 / (res["GRBM_GUI_ACTIVE"][-1] / 8)
     print(json.dumps(res))
 
 
