@@ -325,6 +325,15 @@ int rt_debug_waves(int device, uint64_t* out, size_t n_waves);
  * counts.  Timing only: the bits never depend on it. */
 int rt_steal_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2);
 
+/* A device's one-time start-up, done ahead of the first render so that a
+ * one-frame process (-main, raytracing.clj:95-177) can overlap it with its
+ * own work (rt_main starts it on a thread at process start): the device
+ * context, the kernels' code object, the NULL stream's hardware queue and
+ * the runtime's staging for pageable copies.  out_ms4 (nullable) = the
+ * milliseconds of those four steps.  Idempotent; rt_render does the same
+ * work lazily when it was not called. */
+int rt_prepare(int device, double* out_ms4);
+
 int rt_device_count(void);
 const char* rt_last_error(void);
 const char* rt_version(void);

@@ -115,12 +115,26 @@ extern "C" int rt_camera_setup(int image_width, int image_height, double vfov,
 extern "C" int rt_quantize(const float* lin, uint8_t* out, size_t n) {
   clear_error();
   if ((!lin || !out) && n) return set_error(RT_E_ARG, "rt_quantize: NULL argument");
-  for (size_t i = 0; i < n; ++i) {
-    const double c = lin[i];
-    const double g = c > 0 ? std::sqrt(c) : 0.0;              // linear->gamma (:21-22)
-    const double cl = std::min(0.999, std::max(g, 0.0));      // clamp (:19), NaN -> 0 below
-    const int q = static_cast<int>(256 * cl);                 // (int (* 256 ...)) (:25)
-    out[i] = static_cast<uint8_t>(std::isnan(c) ? 0 : q);
+  auto run = [lin, out](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      const double c = lin[i];
+      const double g = c > 0 ? std::sqrt(c) : 0.0;              // linear->gamma (:21-22)
+      const double cl = std::min(0.999, std::max(g, 0.0));      // clamp (:19), NaN -> 0 below
+      const int q = static_cast<int>(256 * cl);                 // (int (* 256 ...)) (:25)
+      out[i] = static_cast<uint8_t>(std::isnan(c) ? 0 : q);
+    }
+  };
+  // a frame of millions of channels on a few host threads (C1's 2.43 M: 4.4
+  // ms on one); every channel is computed alone, so the split changes nothing
+  const size_t kChunk = size_t{1} << 19;
+  const int nt = static_cast<int>(std::min<size_t>(8, (n + kChunk - 1) / kChunk));
+  if (nt <= 1) {
+    run(0, n);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(run, n * t / nt, n * (t + 1) / nt);
+    run(0, n / nt);
+    for (auto& x : th) x.join();
   }
   return RT_OK;
 }

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <climits>
 #include <cstdlib>
@@ -3090,6 +3091,46 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     sch->ready = true;
   }
   HIP_TRY(hipGetLastError());
+  return RT_OK;
+}
+
+// A device's start-up ahead of the first render (rt.h): the context, the
+// kernels' code object (loaded for the device on a function lookup), the NULL
+// stream's first work (its hardware queue) and a small pageable D2H copy (the
+// runtime's staging for pageable transfers, which the first frame's gather
+// otherwise pays).  Each part timed on the host.
+extern "C" int rt_prepare(int device, double* out_ms4) {
+  clear_error();
+  using Clk = std::chrono::steady_clock;
+  auto ms = [](Clk::time_point a, Clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return set_error(RT_E_NODEV, "rt_prepare: device " + std::to_string(device) + " not available");
+  const auto t0 = Clk::now();
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipFree(nullptr));
+  const auto t1 = Clk::now();
+  hipFuncAttributes fa{};
+  HIP_TRY(hipFuncGetAttributes(&fa, variant_table(16).fn));
+  const auto t2 = Clk::now();
+  constexpr size_t kProbe = 64 * 1024;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, kProbe));
+  hipError_t e = hipMemsetAsync(d, 0, kProbe, nullptr);
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+  const auto t3 = Clk::now();
+  std::vector<unsigned char> host(kProbe);
+  if (e == hipSuccess) e = hipMemcpy(host.data(), d, kProbe, hipMemcpyDeviceToHost);
+  const auto t4 = Clk::now();
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e, "rt_prepare");
+  if (out_ms4) {
+    out_ms4[0] = ms(t0, t1);
+    out_ms4[1] = ms(t1, t2);
+    out_ms4[2] = ms(t2, t3);
+    out_ms4[3] = ms(t3, t4);
+  }
   return RT_OK;
 }
 

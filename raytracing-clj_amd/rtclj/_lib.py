@@ -78,6 +78,7 @@ SIGNATURES = {
     "rt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     "rt_ppm_to_png": (C.c_int, [C.c_char_p, C.c_char_p]),
     "rt_rows_out": (C.c_int, [C.POINTER(rt_params)]),
+    "rt_prepare": (C.c_int, [C.c_int, C.POINTER(C.c_double)]),
     "rt_scene_reference": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_float), C.c_int]),
     "rt_scene_cover": (C.c_int, [C.c_int, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_int),
                                  C.POINTER(C.c_float), C.c_int]),
