@@ -89,10 +89,13 @@ struct alignas(16) KArgs {
   // workgroup each, every later tile is `split` workgroups, one contiguous
   // sample range each, whose integer pixel sums go to part[split index]
   // (finalize_kernel adds them up)
-  unsigned long long* part;  // [split][rows_out][width][3]
+  unsigned long long* part;  // [rows_out][width][3]: the split tiles' integer sums (atomics; zero between launches)
   int tiles_x;               // 8 x 8 tiles per tile row
-  int n_whole, split;
-  int split_k0[65];          // first sample of each split (split_k0[split] = spp)
+  int n_whole, split;        // uniform splits: unit v >= n_whole is split v % split of order position v / split
+  // cost-balanced splits (nullable): unit n_whole + u is samples [k * spp / s,
+  // (k + 1) * spp / s) of tile x, with y = k | s << 8 (x < 0: no unit); the
+  // plan_kernel of the previous launch of the shape made it from the record
+  const int2* unit_tab;
   // n / d as the high half of n * m, m = ceil(2^64 / d) (magic64; m = 0 for
   // d = 1: n itself), exact for every 32-bit n: the kernel's loop divides
   // nothing, so no division has its reciprocal set-up hoisted into loop
@@ -470,18 +473,27 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
 
   // the unit: a whole tile or one sample split of a tile at the order's end
   // (own), or a stolen sample range [first, s_lim) of a whole tile
-  int tile, split_ix = 0, first = 0;
+  int tile, split_ix = 0, first = 0, nsplit = 1;
   bool split = false;
   if (own) {
     int pos = unit;
     split = unit >= ka->n_whole;
-    if (split) {
-      const int v = unit - ka->n_whole;
-      const int t = v / ka->split;
-      pos = ka->n_whole + t;
-      split_ix = v - t * ka->split;
+    if (split && ka->unit_tab) {   // a cost-balanced split
+      const int2 u = ka->unit_tab[unit - ka->n_whole];
+      if (u.x < 0) return;   // (the plan used fewer units than the grid has)
+      tile = u.x;
+      split_ix = u.y & 255;
+      nsplit = u.y >> 8;
+    } else {
+      if (split) {
+        const int v = unit - ka->n_whole;
+        const int t = v / ka->split;
+        pos = ka->n_whole + t;
+        split_ix = v - t * ka->split;
+        nsplit = ka->split;
+      }
+      tile = ka->tile_order ? ka->tile_order[pos] : pos;
     }
-    tile = ka->tile_order ? ka->tile_order[pos] : pos;
   } else {
     tile = sgpr(s_unit[0]);
     first = sgpr(s_unit[1]);
@@ -507,8 +519,8 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
 
   // the unit's samples [k0, k0 + cnt) of each pixel
-  const int k0 = split ? ka->split_k0[split_ix] : 0;
-  const int cnt = split ? ka->split_k0[split_ix + 1] - k0 : ka->spp;
+  const int k0 = split ? static_cast<int>(static_cast<int64_t>(split_ix) * ka->spp / nsplit) : 0;
+  const int cnt = split ? static_cast<int>(static_cast<int64_t>(split_ix + 1) * ka->spp / nsplit) - k0 : ka->spp;
   // pool index j -> (pixel q = j % npx, sample k0 + j / npx); the next free
   // index is `base`.  j / npx by a 64-bit magic (exact for every 32-bit j);
   // q / vw by multiply-high (exact: q < 64, vw <= 8)
@@ -1587,8 +1599,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
     ke->out[e] = ke->realm ? tot * (1.0f / inv) : tot / inv;
   };
-  if (split) {   // one split's integer sum; finalize_kernel adds the splits (order-free)
-    if (t < npx * 3) ke->part[static_cast<size_t>(split_ix) * ke->rows_out * ke->width * 3 + out_index(t)] = s_acc[t];
+  if (split) {   // one split's integer sums, added to the tile's (order-free); finalize_kernel converts them
+    if (t < npx * 3 && s_acc[t])
+      __hip_atomic_fetch_add(&ke->part[out_index(t)], s_acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if (alone) {   // every sample of the tile was this workgroup's
     if (t < npx * 3) write_mean(out_index(t), s_acc[t]);
   } else {
@@ -1747,15 +1760,24 @@ __global__ __launch_bounds__(kSortThreads, 6) void sorted_kernel(const KArgs a) 
   for (int i = threadIdx.x; i < a.bvh_blob_f4; i += kSortThreads) s_geo[i] = a.bvh_blob[i];
   if (ka->tile_cost) st_t0 = __builtin_amdgcn_s_memrealtime();
   // the unit: a whole tile, or one sample split of a tile (as trace_kernel)
-  int pos = unit, split_ix = 0;
+  int pos = unit, split_ix = 0, nsplit = 1, tile;
   const bool split = unit >= ka->n_whole;
-  if (split) {
-    const int v = unit - ka->n_whole;
-    const int t = v / ka->split;
-    pos = ka->n_whole + t;
-    split_ix = v - t * ka->split;
+  if (split && ka->unit_tab) {
+    const int2 u = ka->unit_tab[unit - ka->n_whole];
+    if (u.x < 0) return;
+    tile = u.x;
+    split_ix = u.y & 255;
+    nsplit = u.y >> 8;
+  } else {
+    if (split) {
+      const int v = unit - ka->n_whole;
+      const int t = v / ka->split;
+      pos = ka->n_whole + t;
+      split_ix = v - t * ka->split;
+      nsplit = ka->split;
+    }
+    tile = ka->tile_order ? ka->tile_order[pos] : pos;
   }
-  const int tile = ka->tile_order ? ka->tile_order[pos] : pos;
   const int tby = tile / ka->tiles_x, tbx = tile - tby * ka->tiles_x;
   const int qx0 = tbx * kTile, qy0 = tby * kSortTH;
   const int vw = max(0, min(kTile, ka->width - qx0));
@@ -1772,8 +1794,8 @@ __global__ __launch_bounds__(kSortThreads, 6) void sorted_kernel(const KArgs a) 
     return mix32(a.key ^ mix32(static_cast<uint32_t>(y) * static_cast<uint32_t>(a.width) + static_cast<uint32_t>(x)));
   };
   const float cx = a.cam[0], cy = a.cam[1], cz = a.cam[2];
-  const int k0 = split ? ka->split_k0[split_ix] : 0;
-  const int cnt = split ? ka->split_k0[split_ix + 1] - k0 : ka->spp;
+  const int k0 = split ? static_cast<int>(static_cast<int64_t>(split_ix) * ka->spp / nsplit) : 0;
+  const int cnt = split ? static_cast<int>(static_cast<int64_t>(split_ix + 1) * ka->spp / nsplit) - k0 : ka->spp;
   const int pool = (cnt > 0 && ka->max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
@@ -2179,7 +2201,7 @@ __global__ __launch_bounds__(kSortThreads, 6) void sorted_kernel(const KArgs a) 
     const int px = qx0 + (fp - qy * vw), ro = qy0 + qy;
     const size_t e = (static_cast<size_t>(ro) * ke->width + px) * 3 + ch;
     if (split) {
-      ke->part[static_cast<size_t>(split_ix) * ke->rows_out * ke->width * 3 + e] = s_acc[t];
+      if (s_acc[t]) __hip_atomic_fetch_add(&ke->part[e], s_acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       const float tot = static_cast<float>(s_acc[t]) * 0x1p-24f;
       const float inv = static_cast<float>(ke->spp > 0 ? ke->spp : 1);
@@ -2236,11 +2258,12 @@ __global__ __launch_bounds__(1024) void order_kernel(unsigned* __restrict__ cost
 }
 
 // The split tiles' pixels (order positions [n_whole, n_tiles)): the sum of
-// their splits' integer sums (exact, any order), then the unsplit epilogue's
-// conversion: RN(float(sum)) * 2^-24, / spp (realm: * (1/spp)).  One block
-// per split tile, thread t = tile row * 24 + x * 3 + channel.
-__global__ __launch_bounds__(384) void finalize_kernel(const unsigned long long* __restrict__ part,
-                                                        const int* __restrict__ order, int n_whole, int split,
+// their splits' integer sums (added by the splits' atomics: exact, any
+// order), then the unsplit epilogue's conversion: RN(float(sum)) * 2^-24,
+// / spp (realm: * (1/spp)); the sums are zeroed for the next launch.  One
+// block per split tile, thread t = tile row * 24 + x * 3 + channel.
+__global__ __launch_bounds__(384) void finalize_kernel(unsigned long long* __restrict__ part,
+                                                        const int* __restrict__ order, int n_whole,
                                                         int tiles_x, int tile_h, int width, int rows,
                                                         float* __restrict__ out, int spp, int realm) {
   const int pos = n_whole + static_cast<int>(blockIdx.x);
@@ -2250,13 +2273,83 @@ __global__ __launch_bounds__(384) void finalize_kernel(const unsigned long long*
   const int row = t / (kTile * 3), col = t - row * (kTile * 3);
   const int y = tby * tile_h + row, x3 = tbx * kTile * 3 + col;
   if (row >= tile_h || y >= rows || x3 >= width * 3) return;
-  const size_t n = static_cast<size_t>(rows) * width * 3;
   const size_t e = static_cast<size_t>(y) * width * 3 + x3;
-  unsigned long long sum = 0;
-  for (int s = 0; s < split; ++s) sum += part[static_cast<size_t>(s) * n + e];
+  const unsigned long long sum = part[e];
+  part[e] = 0ull;
   const float tot = static_cast<float>(sum) * 0x1p-24f;
   const float inv = static_cast<float>(spp > 0 ? spp : 1);
   out[e] = realm ? tot * (1.0f / inv) : tot / inv;
+}
+
+// Cost-balanced splits: the next split launch of the shape deals its U units
+// to the tiles in proportion to their recorded cost (the decayed record
+// order_kernel has just sorted and halved), so that units cost about the
+// same and the launch does not end on a few long ones (a uniform split of
+// C1's 8-GPU shard left units of 330-360 us against a 259 us mean in the
+// launch's tail: DESIGN.md §6).  Tile at order position p gets
+// s_p = min(smax, 1 + floor(cost_p (U - n) / C)) units, the U - sum s units
+// left go one each to the first positions, and unit u of the plan is
+// {tile, k | s << 8}: samples [k spp / s, (k + 1) spp / s).  Units the clamps
+// leave over are {-1, 0}.  One block.
+__global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__ cost, const int* __restrict__ order,
+                                                     int n, int U, int smax, int2* __restrict__ units) {
+  __shared__ unsigned long long s_tot;
+  __shared__ int s_part[1024];
+  __shared__ int s_left;
+  const int tid = static_cast<int>(threadIdx.x);
+  const int per = (n + 1023) / 1024;
+  const int p0 = min(n, tid * per), p1 = min(n, p0 + per);
+  if (tid == 0) s_tot = 0ull;
+  __syncthreads();
+  unsigned long long my = 0;
+  for (int p = p0; p < p1; ++p) my += cost[order[p]];
+  if (my) atomicAdd(&s_tot, my);
+  __syncthreads();
+  const unsigned long long tot = s_tot;
+  const int spare = max(0, U - n);
+  auto raw = [&](int p) {
+    const long long c = static_cast<long long>(cost[order[p]]);
+    const long long extra = tot ? (c * spare) / static_cast<long long>(tot) : spare / max(n, 1);
+    return static_cast<int>(min<long long>(smax, 1 + extra));
+  };
+  int sum = 0;
+  for (int p = p0; p < p1; ++p) sum += raw(p);
+  s_part[tid] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+    for (int i = 0; i < 1024; ++i) t += s_part[i];
+    s_left = max(0, U - t);
+  }
+  __syncthreads();
+  const int left = s_left;
+  auto fin = [&](int p) {
+    const int r = raw(p);
+    return r + ((p < left && r < smax) ? 1 : 0);
+  };
+  sum = 0;
+  for (int p = p0; p < p1; ++p) sum += fin(p);
+  __syncthreads();
+  s_part[tid] = sum;
+  __syncthreads();
+  if (tid == 0) {   // exclusive prefix of the threads' unit counts (1024 adds)
+    int run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int v = s_part[i];
+      s_part[i] = run;
+      run += v;
+    }
+    s_left = run;   // units used
+  }
+  __syncthreads();
+  int base = s_part[tid];
+  for (int p = p0; p < p1; ++p) {
+    const int sp = fin(p);
+    const int tile = order[p];
+    for (int k = 0; k < sp; ++k) units[base + k] = make_int2(tile, k | (sp << 8));
+    base += sp;
+  }
+  for (int u = s_left + tid; u < U; u += 1024) units[u] = make_int2(-1, 0);
 }
 
 // ------------------------------------------------------------- host ------
@@ -2410,6 +2503,9 @@ struct Schedule {
   unsigned long long* stealc = nullptr; // [helpers that got samples, their first samples] since rt_steal_stats
   unsigned epoch = 0;                   // launches with sharing on this stream (mod 2^16, 1 .. 65535)
   bool epoch_started = false;
+  int2* units = nullptr;                // cost-balanced split plan (plan_kernel) of the next split launch
+  int units_cap = 0;
+  int plan_units = -1;                  // the plan's unit count (-1: none)
 };
 constexpr int kSchedStreams = 8;
 struct ScheduleSet {
@@ -2425,6 +2521,7 @@ struct ScheduleSet {
     if (e.sum) (void)hipFree(e.sum);
     if (e.owner) (void)hipFree(e.owner);
     if (e.stealc) (void)hipFree(e.stealc);
+    if (e.units) (void)hipFree(e.units);
     e = Schedule{};
   }
   void release() {
@@ -2924,20 +3021,22 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   a.split = split;
   a.n_whole = n_whole;
-  for (int k = 0; k <= split; ++k) a.split_k0[k] = static_cast<int>(static_cast<int64_t>(k) * p->spp / split);
   a.rt_magic = magic64(a.row_tile);
   const int64_t n_units64 = n_whole + static_cast<int64_t>(n_tiles - n_whole) * split;
   if (n_units64 > INT_MAX) return set_error(RT_E_ARG, "rt_launch: frame too large");
   const int n_units = static_cast<int>(n_units64);
   const size_t n_elems = static_cast<size_t>(rows) * p->width * 3;
   if (split > 1) {
-    const size_t need = n_elems * split;
+    // the split tiles' integer sums: one u64 per channel, added to by the
+    // splits, converted and zeroed by finalize_kernel
+    const size_t need = n_elems;
     if (sch->part_cap < need) {   // grow: this stream's kernels may still read the old buffer
       HIP_TRY(hipStreamSynchronize(stream));
       if (sch->part) (void)hipFree(sch->part);
       sch->part = nullptr;
       sch->part_cap = 0;
       HIP_TRY(hipMalloc(&sch->part, need * sizeof(unsigned long long)));
+      HIP_TRY(hipMemsetAsync(sch->part, 0, need * sizeof(unsigned long long), stream));
       sch->part_cap = need;
     }
     a.part = sch->part;
@@ -2977,6 +3076,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     }
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
+    // a split launch in the recorded order: the cost-balanced units the
+    // previous launch of the shape planned, when it planned this many
+    // (RTCLJ_SPLIT_PLAN=0: uniform splits)
+    if (split > 1 && sch->ready && sch->plan_units == n_units - n_whole && env_int("RTCLJ_SPLIT_PLAN", 1, 0) != 0)
+      a.unit_tab = sch->units;
     // the costs decay (order_kernel halves them after sorting): zeroed only
     // when this launch shape starts a new history
     if (!sch->ready) HIP_TRY(hipMemsetAsync(sch->cost, 0, n_tiles * sizeof(unsigned), stream));
@@ -3073,11 +3177,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   void* args[] = {&a};
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
   if (split > 1) {
-    const unsigned long long* part = a.part;
+    unsigned long long* part = a.part;
     const int* order = a.tile_order;
-    int nw = n_whole, sp = split, tx = gx, tht = th, w = p->width, nr = rows, spp = p->spp, realm = a.realm;
+    int nw = n_whole, tx = gx, tht = th, w = p->width, nr = rows, spp = p->spp, realm = a.realm;
     float* out = d_out;
-    void* fargs[] = {&part, &order, &nw, &sp, &tx, &tht, &w, &nr, &out, &spp, &realm};
+    void* fargs[] = {&part, &order, &nw, &tx, &tht, &w, &nr, &out, &spp, &realm};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&finalize_kernel), dim3(n_tiles - n_whole), dim3(kTile * 3 * th),
                             fargs, 0, stream));
   }
@@ -3089,6 +3193,25 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     void* sargs[] = {&cost, &order, &n};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
     sch->ready = true;
+    if (split > 1 && n_whole == 0) {
+      // the next split launch's cost-balanced units, from this record
+      const int U = n_units;
+      if (sch->units_cap < U) {   // grow: this stream's kernels may still read the old plan
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (sch->units) (void)hipFree(sch->units);
+        sch->units = nullptr;
+        sch->units_cap = 0;
+        HIP_TRY(hipMalloc(&sch->units, U * sizeof(int2)));
+        sch->units_cap = U;
+      }
+      int2* units = sch->units;
+      int Uk = U, smax = std::min(p->spp, kSplitMax);
+      void* pargs[] = {&cost, &order, &n, &Uk, &smax, &units};
+      HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&plan_kernel), dim3(1), dim3(1024), pargs, 0, stream));
+      sch->plan_units = U;
+    } else {
+      sch->plan_units = -1;
+    }
   }
   HIP_TRY(hipGetLastError());
   return RT_OK;

@@ -270,3 +270,29 @@ def test_streamed_frames_in_flight_are_bit_exact(env):
     with pytest.raises(RTError):
         R.render(sc, cam, 64, 36, spp=2, flags=RT_FLAG_STREAMED)
 
+
+
+def test_cost_balanced_splits_are_bit_exact(env, split_env, monkeypatch):
+    """Split launches in the recorded order run the units the previous
+    launch's plan_kernel dealt by tile cost (a heavy tile gets more, shorter
+    sample ranges; units the clamps leave over exit): the unsplit bits, with
+    the plan on and off (RTCLJ_SPLIT_PLAN=0), across spp changes that keep
+    the unit count (a plan made for spp 24 run at spp 7: some units empty)
+    and that change it (the plan is then not used)."""
+    from rtclj import scenes
+    sc = env[0]
+    w, h = 200, 112
+    cam = scenes.cover_camera(w, h)
+    split_env(1)
+    want = {spp: _launch(env, cam, w, h, spp) for spp in (24, 7, 5)}
+    for plan in ("1", "0"):
+        monkeypatch.setenv("RTCLJ_SPLIT_PLAN", plan)
+        split_env(4)
+        for spp in (24, 24, 24, 7, 7, 24):
+            got = _launch(env, cam, w, h, spp)
+            assert np.array_equal(got, want[spp]), (plan, spp)
+        split_env(8)
+        for spp in (24, 24, 5, 24, 24):   # spp 5: 5 splits, another unit count
+            got = _launch(env, cam, w, h, spp)
+            assert np.array_equal(got, want[spp]), (plan, spp)
+    monkeypatch.delenv("RTCLJ_SPLIT_PLAN")
