@@ -2852,14 +2852,10 @@ static int dbg_buffers(int device, unsigned long long** dbg, unsigned long long*
 static uint64_t magic64(int d) { return d <= 1 ? 0 : ~0ull / static_cast<uint64_t>(d) + 1ull; }
 
 // Sample split (rt_launch): split every tile of a launch with fewer tiles
-// than kSplitRounds x (resident workgroups), into enough splits to reach that
+// than kSplitRounds (RTCLJ_SPLIT_ROUNDS, default 3) x (resident workgroups), into enough splits to reach that
 // (at most kSplitMax).  tools/shard_time.py on C1's 1/2/4/8-GPU shards
 // (profiles/r02/shard_split_rounds.txt): 3-4 rounds best (8 GPUs: 5.88x at 3,
 // 5.72x at 4, 5.30x at 6, 3.96x at 16; unsplit 2.57x)
-static const int kSplitRounds = [] {
-  const char* e = std::getenv("RTCLJ_SPLIT_ROUNDS");
-  return e ? std::max(1, std::atoi(e)) : 3;
-}();
 constexpr int kSplitMax = 64;
 
 // Tile sharing, A/B knobs read at every launch:
@@ -2870,6 +2866,7 @@ static int env_int(const char* name, int dflt, int lo) {
   const char* e = std::getenv(name);
   return e ? std::max(lo, std::atoi(e)) : dflt;
 }
+static int split_rounds() { return env_int("RTCLJ_SPLIT_ROUNDS", 3, 1); }   // (kSplitRounds above)
 
 // workgroups device `device` holds at once for kernel fn with `lds` bytes of
 // dynamic LDS (CUs x the occupancy query), cached per (device, fn, lds)
@@ -3005,7 +3002,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       split = std::max(1, std::atoi(e));
     } else {
       const int slots = launch_slots(ds->device, v.fn, lds, v.threads);
-      const int64_t want = static_cast<int64_t>(kSplitRounds) * slots;
+      const int64_t want = static_cast<int64_t>(split_rounds()) * slots;
       if (slots > 0 && n_tiles < want) {
         split = static_cast<int>((want + n_tiles - 1) / n_tiles);
         // frames in flight: the next frame fills this launch's tail, so two
@@ -3076,10 +3073,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     }
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
-    // a split launch in the recorded order: the cost-balanced units the
-    // previous launch of the shape planned, when it planned this many
-    // (RTCLJ_SPLIT_PLAN=0: uniform splits)
-    if (split > 1 && sch->ready && sch->plan_units == n_units - n_whole && env_int("RTCLJ_SPLIT_PLAN", 1, 0) != 0)
+    // a split launch in the recorded order: with RTCLJ_SPLIT_PLAN=1, the
+    // cost-balanced units the previous launch of the shape planned (when it
+    // planned this many).  Off by default: C1's 8-GPU shard 1.10-1.15 ms
+    // against 0.99-1.02 with uniform splits, the 4-GPU one 1.93 vs 1.69
+    // (profiles/r04/split_plan/; round 2's cost-sized splits lost the same
+    // way): a heavy tile's many short pools each end with idle lanes.
+    if (split > 1 && sch->ready && sch->plan_units == n_units - n_whole && env_int("RTCLJ_SPLIT_PLAN", 0, 0) != 0)
       a.unit_tab = sch->units;
     // the costs decay (order_kernel halves them after sorting): zeroed only
     // when this launch shape starts a new history
@@ -3193,7 +3193,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     void* sargs[] = {&cost, &order, &n};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
     sch->ready = true;
-    if (split > 1 && n_whole == 0) {
+    if (split > 1 && n_whole == 0 && env_int("RTCLJ_SPLIT_PLAN", 0, 0) != 0) {
       // the next split launch's cost-balanced units, from this record
       const int U = n_units;
       if (sch->units_cap < U) {   // grow: this stream's kernels may still read the old plan
