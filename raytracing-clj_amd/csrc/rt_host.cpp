@@ -157,19 +157,26 @@ extern "C" int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int
     return t;
   }();
   const std::string head = "P3\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
+  bool ok = std::fwrite(head.data(), 1, head.size(), f) == head.size();
+  // formatted a block of pixels at a time into a buffer that stays in cache
+  // (at most "255 255 255\n", 12 bytes, a pixel)
+  constexpr size_t kBlock = 16384;
+  static thread_local std::unique_ptr<char[]> buf(new char[kBlock * 12]);
   const size_t npx = static_cast<size_t>(width) * height;
-  std::vector<char> buf(head.size() + npx * 12);   // at most "255 255 255\n" a pixel
-  char* o = buf.data();
-  std::memcpy(o, head.data(), head.size());
-  o += head.size();
-  for (size_t i = 0; i < 3 * npx; ++i) {
-    const Dec& d = dec[rgb[i]];
-    std::memcpy(o, d.s, 4);   // (the table entry's 4 bytes; the separator overwrites what follows the digits)
-    o += d.len;
-    *o++ = (i % 3 == 2) ? '\n' : ' ';
+  for (size_t b = 0; ok && b < npx; b += kBlock) {
+    const size_t e = std::min(npx, b + kBlock);
+    char* o = buf.get();
+    for (size_t i = b; i < e; ++i) {
+      for (int c = 0; c < 3; ++c) {
+        const Dec& d = dec[rgb[3 * i + c]];
+        std::memcpy(o, d.s, 4);   // (the entry's 4 bytes; the separator overwrites what follows the digits)
+        o += d.len;
+        *o++ = c == 2 ? '\n' : ' ';
+      }
+    }
+    const size_t nb = static_cast<size_t>(o - buf.get());
+    ok = std::fwrite(buf.get(), 1, nb, f) == nb;
   }
-  const size_t nb = static_cast<size_t>(o - buf.data());
-  const bool ok = std::fwrite(buf.data(), 1, nb, f) == nb;
   std::fclose(f);
   return ok ? RT_OK : set_error(RT_E_IO, std::string("rt_write_ppm: short write to ") + path);
 }
