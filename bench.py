@@ -61,7 +61,7 @@ def metric_for(width, height, spp, depth):
     return f"Mray-samples/sec at {width}×{height}×{spp}spp depth{depth}; achieved HBM GB/s vs peak"
 
 # committed rocprofv3 PMC passes of the current build (profiles/pmc.sh), per workload
-PMC_DIRS = {"c1": ROOT / "profiles" / "r03" / "pmc_c1", "c4": ROOT / "profiles" / "r03" / "pmc_c4"}
+PMC_DIRS = {"c1": ROOT / "profiles" / "r04" / "pmc_c1", "c4": ROOT / "profiles" / "r04" / "pmc_c4"}
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
