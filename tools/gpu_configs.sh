@@ -6,7 +6,7 @@ step() { local n=$1 t=$2; shift 2; echo "== $n"; timeout -k 10 $t "$@" > $OUT/$n
 B="python bench.py --cpu-baseline off --e2e off"
 step c2 600 $B --workload c2
 step c3 600 $B --workload c3
-step c4 900 $B --workload c4 --steps 2 --warmup 1
+step c4 900 $B --workload c4 --steps 2 --warmup 1 --pipelined off
 for f in c2 c3 c4; do tail -1 $OUT/$f.log > $OUT/$f.json; done
 step shard_c3 600 python tools/shard_time.py --workload c3 --reps 3 --worlds 1 8
 step shard_c4 900 python tools/shard_time.py --workload c4 --reps 2 --worlds 1 8
