@@ -96,6 +96,9 @@ def parse():
                     help="also time the same K frames with the other basis (2 frames in flight if --inflight "
                          "is 1, else 1), reported beside `value` at every N (single_frame / pipelined); "
                          "off for rocprof runs, whose kernel averages must be the single frame's")
+    ap.add_argument("--sustained", type=float, default=None,
+                    help="seconds of back-to-back single-stream frames after the timed steps, reported as "
+                         "`sustained` (clocks and power under a long load; default 5 for c1, 0 otherwise)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
@@ -107,6 +110,8 @@ def parse():
         a.steps = 100 if a.workload == "c1" else 5
     if a.warmup is None:
         a.warmup = 5 if a.workload == "c1" else 1
+    if a.sustained is None:
+        a.sustained = 5.0 if a.workload == "c1" else 0.0
     return a
 
 
@@ -589,6 +594,28 @@ def main():
     samples_total = sum(r["samples"] for r in per_rank)
     kern_avg_ms = mine["kernel_ms_avg"]
     summary = rank_summary(per_rank, inflight, other_nf, a.steps, a.warmup)
+    # sustained load: as many single-stream frames as fit the requested seconds
+    # at the slowest rank's rate, every rank at once
+    sustained = None
+    if a.sustained > 0:
+        frames = max(1, int(a.sustained * 1e3 / max(r["ms_per_frame"] for r in per_rank)))
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            step(0, p)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        barrier()
+        els = [el]
+        if world > 1:
+            els = [None] * world
+            dist.all_gather_object(els, el)
+        sustained = {"seconds": max(els), "frames": frames,
+                     "value": sum(r["rows"] for r in per_rank) * W * spp * frames / max(els) / 1e6,
+                     "unit": "Mray-samples/s", "ms_per_frame": max(els) / frames * 1e3,
+                     "note": "back-to-back frames on one stream per rank after the timed steps, for the "
+                             "requested seconds: the rate under a long load (clocks, power)"}
 
     res = None
     if rank == 0:
@@ -671,7 +698,7 @@ def main():
             "segments_per_sample": seg_per_sample, "samples_per_step": samples_total / a.steps,
             "kernel": "rtclj::trace_kernel<SRC,SCAN,STATS> (default: BVH with 4-body leaves in LDS, 8x8-pixel "
                       "sample pool per 256-thread workgroup, fixed-point colour sums in LDS)",
-            "end_to_end": None, "cpu_baseline": None, "parity": None,
+            "sustained": sustained, "end_to_end": None, "cpu_baseline": None, "parity": None,
         }
     if a.e2e == "auto":
         # the product fan-out over world devices, timed on rank 0 while the

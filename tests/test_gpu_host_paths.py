@@ -90,3 +90,30 @@ def test_rt_main_cover_scene(gpu_lib, tmp_path):
     h = R.image_height(160)
     ref, _ = _mirror_q8(oracle.MODE_MIRROR32, scenes.cover(11), scenes.cover_camera(160, h), 160, h, 4, 50, seed=9)
     assert np.array_equal(img, ref)
+
+
+def test_prepare_and_first_context_streams(gpu_lib):
+    """rt_prepare (a device's start-up ahead of the first render) reports its
+    four parts and refuses a device that is not there; after rt_cache_clear
+    the first rt_render runs on the device's NULL stream and the next call
+    moves that context to a stream of its own with the tile order it
+    recorded (rt_host.cpp take_ctx): every call renders the same bits, with
+    a new scene uploaded between them."""
+    import ctypes as C
+    import numpy as np
+    from rtclj import raytracing as R, scenes
+    from rtclj._lib import lib
+    ms = (C.c_double * 4)()
+    assert lib.rt_prepare(0, ms) == 0 and all(x >= 0.0 for x in ms)
+    assert lib.rt_prepare(0, None) == 0
+    assert lib.rt_prepare(lib.rt_device_count(), ms) == -5   # RT_E_NODEV
+    lib.rt_cache_clear()
+    sc = scenes.cover(11)
+    w, h = 120, 68
+    cam = scenes.cover_camera(w, h)
+    frames = [R.render(sc, cam, w, h, spp=6, seed=3) for _ in range(2)]
+    other = R.render(R.Scene.from_bodies(R.hittables), R.camera(64, 36, **R.REFERENCE_CAMERA), 64, 36, spp=2)
+    frames += [R.render(sc, cam, w, h, spp=6, seed=3) for _ in range(2)]
+    assert other.shape == (36, 64, 3)
+    assert all(np.array_equal(f, frames[0]) for f in frames[1:])
+    lib.rt_cache_clear()

@@ -23,7 +23,7 @@ for s in $STAGES; do
     bench) run bench 600 python bench.py --steps 20 --warmup 5
            tail -1 "$OUT/bench.log" > "$OUT/bench.json" ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o prof -- \
-               python3 bench.py --steps 20 --warmup 5 --cpu-baseline off --e2e off --stats off --pipelined off ;;
+               python3 bench.py --steps 20 --warmup 5 --cpu-baseline off --e2e off --stats off --pipelined off --sustained 0 ;;
     pmc)   run pmc 900 bash profiles/pmc.sh "$OUT/pmc" ;;
     shard) run shard 300 python tools/shard_time.py --workload c1 --reps 5 --inflight 2 --frames 80
            grep "N=" "$OUT/shard.log" > "$OUT/shard.txt" ;;

@@ -15,7 +15,7 @@ step pmc_c4 900 env PMC_PASSES="waves insts fetch write" bash profiles/pmc.sh $O
 mkdir -p profiles/r04/pmc_c1 profiles/r04/pmc_c4; for w in c1 c4; do cp $OUT/pmc_$w/*.csv profiles/r04/pmc_$w/; done
 step bench 600 python bench.py
 tail -1 $OUT/bench.log > $OUT/bench.json
-step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o prof -- python3 bench.py --cpu-baseline off --e2e off --stats off --pipelined off
+step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o prof -- python3 bench.py --cpu-baseline off --e2e off --stats off --pipelined off --sustained 0
 step dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 3 --cpu-baseline off
 tail -1 $OUT/dist2.log > $OUT/dist2.json
 step dist4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 10 --warmup 3 --cpu-baseline off
