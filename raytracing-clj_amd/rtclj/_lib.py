@@ -103,6 +103,8 @@ SIGNATURES = {
 }
 
 RT_ABI_VERSION = 3   # include/rt.h; the structures above are this revision's
+# functions added within the revision (a build from before them still loads)
+ADDITIVE = {"rt_prepare"}
 
 
 def load(path: Path) -> C.CDLL:
@@ -114,6 +116,8 @@ def load(path: Path) -> C.CDLL:
                           "(or __graft_entry__.build()); there is no CPU fallback")
     dll = C.CDLL(str(path), mode=os.RTLD_NOW | os.RTLD_LOCAL)
     for name, (res, args) in SIGNATURES.items():
+        if name in ADDITIVE and not hasattr(dll, name):
+            continue   # (an older build of the same revision: A/B of library builds)
         fn = getattr(dll, name)
         fn.restype = res
         fn.argtypes = args
