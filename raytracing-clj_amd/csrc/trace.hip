@@ -128,6 +128,7 @@ struct alignas(16) KArgs {
   int share_from;                // units before this one never share (they end long before the launch's tail)
   int steal_min;
   int batch_max;                 // a wave's largest claim on a shared tile (0: by the pool)
+  int lds_batch_max;             // ... on an unshared pool (from the workgroup's LDS counter; >= 64)
   unsigned epoch;                // this launch's (per stream, 1 .. 65535)
   // Drain compaction: a wave whose batches are spent and
   // which holds at most `compact` paths posts them to its siblings through
@@ -1518,7 +1519,10 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         // a shared tile's claims shrink as its pool is spent (guided: an
         // eighth of what is left past this wave's last batch, kShareBatch ..
         // batch_max)
-        const int want = src ? max(kShareBatch, min(kc_batch_max, ((pool - we) >> 3) & ~63)) : 64;
+        // an unshared pool's the same way from its LDS counter, 64 ..
+        // lds_batch_max (read where it is used: no register held for it)
+        const int want = src ? max(kShareBatch, min(kc_batch_max, ((pool - we) >> 3) & ~63))
+                             : max(64, min(kargs_opaque()->lds_batch_max, ((pool - we) >> 3) & ~63));
         const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
         if (lane == leader) {
           if (src) {
@@ -3174,6 +3178,9 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     a.batch_max = env_int("RTCLJ_BATCH_MAX", a.tile_order ? 1024 : 0, 0);
   }
   a.n_units = n_units;
+  // a wave's claims on an unshared pool: guided (an eighth of what is left
+  // past its last batch), 64 .. RTCLJ_LDS_BATCH
+  a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 64, 64));
   void* args[] = {&a};
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
   if (split > 1) {
