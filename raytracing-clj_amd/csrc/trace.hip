@@ -1532,7 +1532,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
             if (g < pool) atomicAdd(&s_cnt, min(pool - g, want));
             atomicMax(&s_join, word_helpers(wd));
           } else {
-            g = atomicAdd(&s_pool_next, 64);
+            g = atomicAdd(&s_pool_next, want);
           }
         }
         g = __builtin_amdgcn_readlane(g, leader);
