@@ -3179,8 +3179,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   a.n_units = n_units;
   // a wave's claims on an unshared pool: guided (an eighth of what is left
-  // past its last batch), 64 .. RTCLJ_LDS_BATCH
-  a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 64, 64));
+  // past its last batch), 64 .. RTCLJ_LDS_BATCH (default 256; fixed 64-index
+  // batches were round 3's: C1 5.960 -> 5.916 ms, C2 287.9 -> 286.1 ms,
+  // profiles/r04/lds_batch/)
+  a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 256, 64));
   void* args[] = {&a};
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
   if (split > 1) {
