@@ -18,6 +18,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -272,6 +275,60 @@ struct Ctx {
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
+
+// rt_render's fan-out threads, kept between calls: a call runs its first
+// device's share on the calling thread and hands the others to idle
+// workers (spawned when none is idle, up to 64, never joined: the pool lives
+// as long as the process), instead of creating and joining a std::thread per
+// device per call.  Tasks never wait on other pool tasks, so a queue longer
+// than the idle workers only delays them.
+class HostPool {
+ public:
+  void run(std::vector<std::function<void()>>& tasks) {
+    if (tasks.empty()) return;
+    struct Latch {
+      std::mutex m;
+      std::condition_variable cv;
+      int left = 0;
+    } latch;
+    latch.left = static_cast<int>(tasks.size()) - 1;
+    if (latch.left > 0) {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 1; i < tasks.size(); ++i)
+        q_.push_back([&tasks, &latch, i] {
+          tasks[i]();
+          std::lock_guard<std::mutex> l2(latch.m);
+          if (--latch.left == 0) latch.cv.notify_all();
+        });
+      const int want = static_cast<int>(q_.size()) - idle_;
+      for (int k = 0; k < want && workers_ < 64; ++k, ++workers_) std::thread([this] { work(); }).detach();
+      cv_.notify_all();
+    }
+    tasks[0]();
+    std::unique_lock<std::mutex> l2(latch.m);
+    latch.cv.wait(l2, [&] { return latch.left == 0; });
+  }
+
+ private:
+  void work() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      ++idle_;
+      cv_.wait(lk, [this] { return !q_.empty(); });
+      --idle_;
+      std::function<void()> t = std::move(q_.front());
+      q_.pop_front();
+      lk.unlock();
+      t();
+      lk.lock();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  int idle_ = 0, workers_ = 0;
+};
+HostPool* g_pool = new HostPool;   // never destroyed (workers may still wait on it at exit)
 
 constexpr int kSceneCache = 4;   // scenes kept per device (least recently used out)
 // idle contexts kept per device: as many as a scene has per-stream schedule
@@ -598,9 +655,10 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
   if (ndev == 1) {
     run_shard(s, c, &shards[0], out_rgb, rows, ntiles, 1, 0);
   } else {
-    std::vector<std::thread> th;
-    for (int d = 0; d < ndev; ++d) th.emplace_back(run_shard, s, c, &shards[d], out_rgb, rows, ntiles, ndev, d);
-    for (auto& t : th) t.join();
+    std::vector<std::function<void()>> tasks;
+    for (int d = 0; d < ndev; ++d)
+      tasks.emplace_back([=, &shards] { run_shard(s, c, &shards[d], out_rgb, rows, ntiles, ndev, d); });
+    g_pool->run(tasks);
   }
   double kms = 0, ksum = 0, ums = 0, gms = 0, d2h = 0;
   uint64_t segs = 0, smp = 0;
