@@ -220,8 +220,8 @@ int rt_scene_cover(int grid, uint64_t seed, float* sphere, int* kind, float* mat
 /* Render into a caller-owned host buffer of linear RGB fp32, row-major,
  * rows_out x width x 3, the mean over spp (compute-pixel's accum/spp,
  * raytracing.clj:155).  Fans out over p->n_devices GPUs inside the call
- * (one host thread per device, interleaved row tiles, host-side gather; no
- * collectives).  tile_first/tile_step must be 0 here.  stats may be NULL.
+ * (a host worker per device from a persistent pool, interleaved row tiles,
+ * each device's rows copied straight into their place; no collectives).  tile_first/tile_step must be 0 here.  stats may be NULL.
  *
  * The device copy of the scene (tables + BVHs) is cached per device by the
  * scene's content (a hash, then a byte compare): a repeated call with the
@@ -231,6 +231,13 @@ int rt_scene_cover(int grid, uint64_t seed, float* sphere, int* kind, float* mat
  * Output bits never depend on the cache. */
 int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p,
               float* out_rgb, size_t out_len, rt_stats* stats);
+
+/* rt_render, then rt_quantize on the device: out_rgb8 (rows_out x width x 3
+ * bytes) holds exactly the bytes rt_quantize gives for rt_render's floats,
+ * the write-color! bytes of the -main loop (raytracing.clj:160-175), at a
+ * quarter of the copy back.  stats->d2h_ms includes the quantiser. */
+int rt_render_u8(const rt_scene* s, const rt_camera* c, const rt_params* p,
+                 uint8_t* out_rgb8, size_t out_len, rt_stats* stats);
 
 /* Drop rt_render's cached device scenes and render contexts (streams,
  * buffers; those not in use by a concurrent call).  Returns the number of
@@ -251,6 +258,13 @@ int rt_scene_free(rt_dscene* ds);
  * stream (splits x rows x width x 3 x 8 bytes).  Bits never depend on it. */
 int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
               float* d_out, uint64_t* d_counters, void* hip_stream);
+
+/* Asynchronous: enqueue rt_quantize on hip_stream's device for n channels
+ * already in HBM (d_lin: n floats, d_out: n bytes, device pointers): the same
+ * bytes as rt_quantize for every float (NaN, infinities and denormals
+ * included), through a table of the 255 float thresholds between bytes that
+ * the host derives from rt_quantize's own arithmetic. */
+int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_stream);
 
 /* Kernel variant selector (all variants give identical bits).  The product
  * library holds: 0 = default (16, or 18 when the 4-body tree's LDS image

@@ -115,17 +115,47 @@ extern "C" int rt_camera_setup(int image_width, int image_height, double vfov,
   return RT_OK;
 }
 
+// one channel's byte (color.clj write-color)
+static inline uint8_t quantize1(float lin) {
+  const double c = lin;
+  const double g = c > 0 ? std::sqrt(c) : 0.0;              // linear->gamma (:21-22)
+  const double cl = std::min(0.999, std::max(g, 0.0));      // clamp (:19), NaN -> 0 below
+  const int q = static_cast<int>(256 * cl);                 // (int (* 256 ...)) (:25)
+  return static_cast<uint8_t>(std::isnan(c) ? 0 : q);
+}
+
+namespace rtclj {
+const float* quantize_thresholds() {
+  // the byte is 0 for NaN and every float <= 0 and non-decreasing over the
+  // positive floats in bit order (sqrt, min, the scale and the truncation
+  // all are), so each threshold is a binary search over [+0, +inf]
+  static const std::vector<float> t = [] {
+    std::vector<float> v(256, -INFINITY);
+    auto of = [](uint32_t b) {
+      float f;
+      std::memcpy(&f, &b, 4);
+      return f;
+    };
+    for (int q = 1; q < 256; ++q) {
+      uint32_t lo = 0, hi = 0x7f800000u;   // byte(lo) < q <= byte(hi) (byte(+inf) = 255)
+      while (hi - lo > 1) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (quantize1(of(mid)) >= q) hi = mid;
+        else lo = mid;
+      }
+      v[q] = of(hi);
+    }
+    return v;
+  }();
+  return t.data();
+}
+}  // namespace rtclj
+
 extern "C" int rt_quantize(const float* lin, uint8_t* out, size_t n) {
   clear_error();
   if ((!lin || !out) && n) return set_error(RT_E_ARG, "rt_quantize: NULL argument");
   auto run = [lin, out](size_t b, size_t e) {
-    for (size_t i = b; i < e; ++i) {
-      const double c = lin[i];
-      const double g = c > 0 ? std::sqrt(c) : 0.0;              // linear->gamma (:21-22)
-      const double cl = std::min(0.999, std::max(g, 0.0));      // clamp (:19), NaN -> 0 below
-      const int q = static_cast<int>(256 * cl);                 // (int (* 256 ...)) (:25)
-      out[i] = static_cast<uint8_t>(std::isnan(c) ? 0 : q);
-    }
+    for (size_t i = b; i < e; ++i) out[i] = quantize1(lin[i]);
   };
   // a frame of millions of channels on a few host threads (C1's 2.43 M: 4.4
   // ms on one); every channel is computed alone, so the split changes nothing
@@ -253,6 +283,8 @@ struct Ctx {
   hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
   float* d_out = nullptr;
   size_t d_cap = 0;           // floats
+  uint8_t* d_u8 = nullptr;    // rt_render_u8's bytes
+  size_t u8_cap = 0;
   uint64_t* d_cnt = nullptr;
   uint64_t* h_cnt = nullptr;  // pinned
   std::vector<const void*> scenes;   // device scenes launched on (their per-stream schedule entries)
@@ -270,6 +302,7 @@ struct Ctx {
     if (e1) (void)hipEventDestroy(e1);
     if (e2) (void)hipEventDestroy(e2);
     if (d_out) (void)hipFree(d_out);
+    if (d_u8) (void)hipFree(d_u8);
     if (d_cnt) (void)hipFree(d_cnt);
     if (h_cnt) (void)hipHostFree(h_cnt);
     if (stream) (void)hipStreamDestroy(stream);
@@ -469,9 +502,10 @@ struct Shard {
 
 // one device's share: scene (cached), launch, D2H of its compacted row
 // tiles straight into their rows of out_rgb (disjoint rows: the shards copy
-// in parallel, each as soon as its own device is done)
-void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb, int rows_total, int ntiles,
-               int nshards, int shard_idx) {
+// in parallel, each as soon as its own device is done).  u8: out_rgb is
+// bytes, quantised on the device after the launch (rt_render_u8)
+void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, bool u8, int rows_total,
+               int ntiles, int nshards, int shard_idx) {
   auto fail = [&](int code) {
     sh->status = code;
     sh->err = rt_last_error();
@@ -513,6 +547,13 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
     e = hipMalloc(&cx->d_out, std::max<size_t>(nfl, 1) * sizeof(float));
     if (e == hipSuccess) cx->d_cap = nfl;
   }
+  if (e == hipSuccess && u8 && cx->u8_cap < nfl) {
+    if (cx->d_u8) (void)hipFree(cx->d_u8);
+    cx->d_u8 = nullptr;
+    cx->u8_cap = 0;
+    e = hipMalloc(&cx->d_u8, std::max<size_t>(nfl, 1));
+    if (e == hipSuccess) cx->u8_cap = nfl;
+  }
   sh->setup_ms = ms_since(t_setup);
   // upload_ms: the part of the upload the call waited for after its set-up
   const auto t_up = Clock::now();
@@ -536,6 +577,10 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
       fail(rc);
     } else {
       e = hipEventRecord(cx->e1, cx->stream);
+      // (u8: the quantiser's few microseconds fall in d2h_ms)
+      if (e == hipSuccess && u8 && nfl) e = static_cast<hipError_t>(quantize_launch(cx->d_out, cx->d_u8, nfl, cx->stream));
+      const void* src = u8 ? static_cast<const void*>(cx->d_u8) : static_cast<const void*>(cx->d_out);
+      const size_t es = u8 ? 1 : sizeof(float);
       // straight into the caller's buffer (measured on MI355X for a C1
       // frame: 0.46-0.52 ms, against 0.53-0.56 ms into pinned staging plus
       // 0.34 ms of host copy, tools/d2h_bench.cpp).  Several shards: the
@@ -544,21 +589,21 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, float* out_rgb,
       // nshards), the image's last tile, if it is short, through a second
       if (e == hipSuccess && nfl) {
         if (nshards == 1) {
-          e = hipMemcpyAsync(out_rgb, cx->d_out, nfl * sizeof(float), hipMemcpyDeviceToHost, cx->stream);
+          e = hipMemcpyAsync(out_rgb, src, nfl * es, hipMemcpyDeviceToHost, cx->stream);
         } else {
           const int T = sh->p.row_tile;
-          const size_t rowb = static_cast<size_t>(sh->p.width) * 3 * sizeof(float);
+          const size_t rowb = static_cast<size_t>(sh->p.width) * 3 * es;
           const int ntile = (ntiles - shard_idx + nshards - 1) / nshards;   // this shard's tiles
           const int t_last = shard_idx + (ntile - 1) * nshards;
           const bool short_last = t_last == ntiles - 1 && rows_total % T != 0;
           const int nfull = ntile - (short_last ? 1 : 0);
           if (nfull > 0)
             e = hipMemcpy2DAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(shard_idx) * T * rowb,
-                                 static_cast<size_t>(nshards) * T * rowb, cx->d_out, T * rowb, T * rowb, nfull,
+                                 static_cast<size_t>(nshards) * T * rowb, src, T * rowb, T * rowb, nfull,
                                  hipMemcpyDeviceToHost, cx->stream);
           if (e == hipSuccess && short_last)
             e = hipMemcpyAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(t_last) * T * rowb,
-                               reinterpret_cast<const char*>(cx->d_out) + static_cast<size_t>(nfull) * T * rowb,
+                               static_cast<const char*>(src) + static_cast<size_t>(nfull) * T * rowb,
                                static_cast<size_t>(rows_total - t_last * T) * rowb, hipMemcpyDeviceToHost, cx->stream);
         }
       }
@@ -609,8 +654,10 @@ extern "C" int rt_cache_clear(void) {
   return dropped;
 }
 
-extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p, float* out_rgb,
-                         size_t out_len, rt_stats* stats) {
+namespace {
+// rt_render and rt_render_u8: out_rgb holds floats or (u8) bytes
+int render(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_rgb, bool u8, size_t out_len,
+           rt_stats* stats) {
   clear_error();
   const auto t0 = Clock::now();
   if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, "rt_render: NULL argument");
@@ -653,11 +700,11 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     sh.rows = rows_out(sh.p);
   }
   if (ndev == 1) {
-    run_shard(s, c, &shards[0], out_rgb, rows, ntiles, 1, 0);
+    run_shard(s, c, &shards[0], out_rgb, u8, rows, ntiles, 1, 0);
   } else {
     std::vector<std::function<void()>> tasks;
     for (int d = 0; d < ndev; ++d)
-      tasks.emplace_back([=, &shards] { run_shard(s, c, &shards[d], out_rgb, rows, ntiles, ndev, d); });
+      tasks.emplace_back([=, &shards] { run_shard(s, c, &shards[d], out_rgb, u8, rows, ntiles, ndev, d); });
     g_pool->run(tasks);
   }
   double kms = 0, ksum = 0, ums = 0, gms = 0, d2h = 0;
@@ -694,5 +741,25 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
     stats->total_ms = ms_since(t0);
     stats->other_ms = stats->total_ms - (sl.upload_ms + sl.setup_ms + sl.enqueue_ms + sl.wait_ms + sl.scatter_ms);
   }
+  return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p, float* out_rgb,
+                         size_t out_len, rt_stats* stats) {
+  return render(s, c, p, out_rgb, false, out_len, stats);
+}
+
+extern "C" int rt_render_u8(const rt_scene* s, const rt_camera* c, const rt_params* p, uint8_t* out_rgb8,
+                            size_t out_len, rt_stats* stats) {
+  return render(s, c, p, out_rgb8, true, out_len, stats);
+}
+
+extern "C" int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_stream) {
+  clear_error();
+  if ((!d_lin || !d_out) && n) return set_error(RT_E_ARG, "rt_quantize_device: NULL argument");
+  if (n == 0) return RT_OK;
+  const hipError_t e = static_cast<hipError_t>(quantize_launch(d_lin, d_out, n, hip_stream));
+  if (e != hipSuccess) return set_error(RT_E_HIP, std::string("rt_quantize_device: ") + hipGetErrorString(e));
   return RT_OK;
 }

@@ -46,4 +46,14 @@ void release_stream_schedules(void* stream, const void* const* scenes, int n);
 // (both streams idle; a scene that already has an entry for `to` keeps it).
 void rebind_stream_schedules(void* from, void* to, const void* const* scenes, int n);
 
+// rt_quantize's byte of one channel as 255 thresholds: t[q] (q = 1..255) is
+// the smallest float whose byte is >= q (t[0] unused), so a channel's byte is
+// the number of thresholds <= it -- exact for every float, NaN included
+// (no comparison holds).  Built once from rt_quantize's own arithmetic
+// (rt_host.cpp); the device quantiser (trace.hip) searches it.
+const float* quantize_thresholds();
+// Enqueue the device quantiser: d_out[i] = rt_quantize's byte of d_lin[i].
+// Returns the launch's hipError_t (0: enqueued).
+int quantize_launch(const float* d_lin, uint8_t* d_out, size_t n, void* stream);
+
 }  // namespace rtclj

@@ -5,10 +5,14 @@
 // instead: realm's body order, camera (no defocus, focal length
 // |look-from - look-at|), height (int (/ ^double 400 ^double 16/9)) = 224 and
 // RT_FLAG_REALM semantics; it writes scene-realm.ppm.  --png also writes the
-// frame as a PNG (rt_write_png; what src/ppm2png.clj produces).
+// frame as a PNG (rt_write_png; what src/ppm2png.clj produces).  The frame
+// is quantised on the device (rt_render_u8: a quarter of the copy back, no
+// host pass); --host-quantize takes rt_render's floats and rt_quantize
+// instead (the same bytes).
 //
 //   rt_main [spp] [depth] [--scene reference|cover] [--realm] [--width W]
 //           [--seed S] [--gpus N] [--out PATH] [--png PATH] [--json]
+//           [--host-quantize]
 // Defaults follow the reference: spp 100, depth 50, width 400, 16:9.
 // --json: one more line, a JSON object of where this one-frame process's time
 // went (the device start-up -- the HIP runtime's first rt_device_count, then
@@ -32,7 +36,7 @@ int main(int argc, char** argv) {
   int spp = 100, depth = 50, width = 400, gpus = 0, grid = 11;
   unsigned long long seed = 1;
   std::string scene = "reference", out, png;
-  bool realm = false, json = false;
+  bool realm = false, json = false, host_quantize = false;
   int pos = 0;
   const auto t_start = std::chrono::steady_clock::now();
   auto ms_since = [](std::chrono::steady_clock::time_point t) {
@@ -77,6 +81,7 @@ int main(int argc, char** argv) {
     else if (a == "--png") png = val();
     else if (a == "--realm") realm = true;
     else if (a == "--json") json = true;
+    else if (a == "--host-quantize") host_quantize = true;
     else if (pos == 0) spp = std::atoi(argv[i]), ++pos;   // (:96)
     else if (pos == 1) depth = std::atoi(argv[i]), ++pos; // (:97)
   }
@@ -126,17 +131,27 @@ int main(int argc, char** argv) {
   p.n_devices = gpus;
   p.flags = realm ? RT_FLAG_REALM : 0;
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<float> lin(static_cast<size_t>(width) * height * 3);
+  const size_t nch = static_cast<size_t>(width) * height * 3;
+  std::vector<uint8_t> q(nch);
   rt_stats st{};
-  if (rt_render(&s, &cam, &p, lin.data(), lin.size(), &st) != RT_OK) {
-    std::fprintf(stderr, "rt_render failed: %s\n", rt_last_error());
-    return 1;
+  double render_ms = 0.0, quantize_ms = 0.0;
+  if (host_quantize) {
+    std::vector<float> lin(nch);
+    if (rt_render(&s, &cam, &p, lin.data(), lin.size(), &st) != RT_OK) {
+      std::fprintf(stderr, "rt_render failed: %s\n", rt_last_error());
+      return 1;
+    }
+    render_ms = ms_since(t0);
+    const auto t_q = std::chrono::steady_clock::now();
+    rt_quantize(lin.data(), q.data(), q.size());
+    quantize_ms = ms_since(t_q);
+  } else {
+    if (rt_render_u8(&s, &cam, &p, q.data(), q.size(), &st) != RT_OK) {
+      std::fprintf(stderr, "rt_render_u8 failed: %s\n", rt_last_error());
+      return 1;
+    }
+    render_ms = ms_since(t0);
   }
-  const double render_ms = ms_since(t0);
-  const auto t_q = std::chrono::steady_clock::now();
-  std::vector<uint8_t> q(lin.size());
-  rt_quantize(lin.data(), q.data(), q.size());
-  const double quantize_ms = ms_since(t_q);
   const auto t_w = std::chrono::steady_clock::now();
   if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK ||
       (!png.empty() && rt_write_png(png.c_str(), q.data(), width, height) != RT_OK)) {
@@ -153,13 +168,13 @@ int main(int argc, char** argv) {
     std::printf(
         "{\"devices_visible\": %d, \"scene_ms\": %.3f, \"device_count_ms\": %.3f, \"prepare_ms\": {\"context\": %.3f, "
         "\"code_object\": %.3f, \"queue\": %.3f, \"pageable_staging\": %.3f}, \"prepare_wait_ms\": %.3f, "
-        "\"render_ms\": %.3f, "
+        "\"render_ms\": %.3f, \"quantize\": \"%s\", "
         "\"quantize_ms\": %.3f, \"write_ms\": %.3f, \"process_ms\": %.3f, \"rt_stats\": {\"total_ms\": %.3f, "
         "\"upload_ms\": %.3f, \"setup_ms\": %.3f, \"enqueue_ms\": %.3f, \"wait_ms\": %.3f, \"scatter_ms\": %.3f, "
         "\"other_ms\": %.3f, \"kernel_ms\": %.3f, \"d2h_ms\": %.3f, \"segments\": %llu, \"samples\": %llu, "
         "\"n_devices\": %d}}\n",
         ndev, scene_ms, device_count_ms, prep_ms[0], prep_ms[1], prep_ms[2], prep_ms[3], prep_wait_ms, render_ms,
-        quantize_ms, write_ms, ms_since(t_start), st.total_ms,
+        host_quantize ? "host" : "device", quantize_ms, write_ms, ms_since(t_start), st.total_ms,
         st.upload_ms, st.setup_ms, st.enqueue_ms, st.wait_ms, st.scatter_ms, st.other_ms, st.kernel_ms, st.d2h_ms,
         static_cast<unsigned long long>(st.segments), static_cast<unsigned long long>(st.samples), st.n_devices);
   return 0;

@@ -2285,6 +2285,29 @@ __global__ __launch_bounds__(384) void finalize_kernel(unsigned long long* __res
   out[e] = realm ? tot * (1.0f / inv) : tot / inv;
 }
 
+// rt_quantize on the device (rt_render_u8, rt_quantize_device): a channel's
+// byte is the number of thresholds t[1..255] <= it (rt_internal.h), found by
+// an 8-step binary search in LDS -- NaN fails every compare and gets 0, as
+// rt_quantize's isnan does.  Streaming: 4 bytes read, 1 written per channel.
+struct QThr {
+  float t[256];
+};
+__global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__ lin, uint8_t* __restrict__ out,
+                                                        size_t n, const QThr q) {
+  __shared__ float s_t[256];
+  s_t[threadIdx.x] = q.t[threadIdx.x];
+  __syncthreads();
+  const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+    const float c = lin[i];
+    int b = 0;
+#pragma unroll
+    for (int step = 128; step > 0; step >>= 1)
+      if (s_t[b + step] <= c) b += step;   // b + step <= 255
+    out[i] = static_cast<uint8_t>(b);
+  }
+}
+
 // Cost-balanced splits: the next split launch of the shape deals its U units
 // to the tiles in proportion to their recorded cost (the decayed record
 // order_kernel has just sorted and halved), so that units cost about the
@@ -2888,6 +2911,24 @@ static int launch_slots(int device, const void* fn, size_t lds, int threads = 25
   cache.push_back({device, fn, lds, cus * per});
   return cus * per;
 }
+
+namespace rtclj {
+int quantize_launch(const float* d_lin, uint8_t* d_out, size_t n, void* stream) {
+  static const QThr thr = [] {
+    QThr t;
+    std::memcpy(t.t, quantize_thresholds(), sizeof t.t);
+    return t;
+  }();
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 4096);
+  QThr q = thr;
+  const float* in = d_lin;
+  uint8_t* out = d_out;
+  void* args[] = {&in, &out, &n, &q};
+  return hipLaunchKernel(reinterpret_cast<const void*>(&quantize_kernel), dim3(static_cast<unsigned>(blocks)),
+                         dim3(256), args, 0, static_cast<hipStream_t>(stream));
+}
+}  // namespace rtclj
 
 extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p, float* d_out,
                          uint64_t* d_counters, void* hip_stream) {

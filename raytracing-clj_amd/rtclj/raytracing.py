@@ -122,7 +122,7 @@ def camera(image_width, image_h, vfov, look_from, look_at, vup, defocus_angle, f
 
 def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50, seed: int = 1,
            n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None,
-           flags: int = 0, library=None, out=None):
+           flags: int = 0, library=None, out=None, u8: bool = False):
     """compute-pixel for every pixel of rows [r0, r1) (default: all), on the GPU.
 
     Returns float32 (rows, width, 3) linear RGB, each pixel the mean of its spp
@@ -130,7 +130,9 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
     `library`: another loaded build of the ABI (rtclj._lib.diag_lib()).
     `out`: a C-contiguous float32 (rows, width, 3) array to render into (a
     renderer drawing frames reuses its framebuffer; a fresh 10 MB array's
-    pages are first touched by the copy into it)."""
+    pages are first touched by the copy into it).
+    `u8`: return write-color!'s bytes instead (rt_render_u8: the frame is
+    quantised on the device; bit-identical to write_color(render(...)))."""
     dll = library if library is not None else lib
     if not isinstance(scene, Scene):
         scene = Scene.from_bodies(scene)
@@ -138,12 +140,16 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
     p = rt_params(width=width, height=height, row_begin=r0, row_end=r1, spp=spp, max_depth=max_depth,
                   seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
     shape = (max(r1 - r0, 0), width, 3)
+    dt = np.uint8 if u8 else np.float32
     if out is None:
-        out = np.empty(shape, np.float32)
-    elif out.shape != shape or out.dtype != np.float32 or not out.flags.c_contiguous:
-        raise ValueError(f"render: out must be C-contiguous float32 {shape}")
+        out = np.empty(shape, dt)
+    elif out.shape != shape or out.dtype != dt or not out.flags.c_contiguous:
+        raise ValueError(f"render: out must be C-contiguous {np.dtype(dt).name} {shape}")
     st = rt_stats()
-    code = dll.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st))
+    if u8:
+        code = dll.rt_render_u8(C.byref(scene.c), C.byref(cam), C.byref(p), u8ptr(out), out.size, C.byref(st))
+    else:
+        code = dll.rt_render(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(st))
     if code < 0:
         raise RTError(code, dll.rt_last_error().decode(errors="replace"))
     if stats is not None:

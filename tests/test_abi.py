@@ -107,6 +107,12 @@ def test_argument_errors():
     assert lib.rt_camera_setup(0, 9, 20.0, None, None, None, 0.0, 1.0, C.byref(rt_camera())) == -1
     assert lib.rt_quantize(None, None, 4) == -1
     assert lib.rt_quantize(None, None, 0) == 0
+    assert lib.rt_quantize_device(None, None, 4, None) == -1
+    assert lib.rt_quantize_device(None, None, 0, None) == 0
+    b8 = (C.c_uint8 * (16 * 9 * 3))()
+    assert lib.rt_render_u8(None, C.byref(cam), C.byref(p), b8, 16 * 9 * 3, None) == -1
+    assert lib.rt_render_u8(C.byref(sc.c), C.byref(cam), C.byref(p_short), b8, 10, None) == -1
+    assert b"out_len" in lib.rt_last_error()
     assert lib.rt_write_ppm(b"/nonexistent-dir/x.ppm", (C.c_uint8 * 3)(), 1, 1) == -6
     bad = rt_scene(-1, None, None, None)
     assert lib.rt_scene_upload(0, C.byref(bad), C.byref(C.c_void_p())) == -1

@@ -66,6 +66,10 @@ def test_rt_main_reference_scene_equals_mirror(gpu_lib, tmp_path):
     assert np.array_equal(img, ref)
     assert abs(_segs_per_sample(out) - sps) < 1e-3
     assert np.array_equal(decode((tmp_path / "scene.png").read_bytes())[0], img)
+    # the frame is quantised on the device (rt_render_u8); rt_render's floats
+    # through rt_quantize on the host write the same file
+    _run(["16", "50", "--out", "host.ppm", "--gpus", "1", "--host-quantize"], tmp_path)
+    assert (tmp_path / "host.ppm").read_bytes() == (tmp_path / "scene.ppm").read_bytes()
 
 
 def test_rt_main_realm_equals_mirror(gpu_lib, tmp_path):
