@@ -10,12 +10,20 @@
  *                            float[] outRgb);
  *   static native int renderWithFlags(... the same ..., int nGpus, int flags,
  *                                     float[] outRgb);   // RT_FLAG_REALM: -M:realm
+ *   static native int renderBytes(... the same ..., int nGpus, int flags,
+ *                                 byte[] outRgb);   // rt_render_u8: write-color!'s bytes
+ *   static native int cameraSetup(int width, int height, double vfov,
+ *                                 double[] lookFrom, double[] lookAt, double[] vup,
+ *                                 double defocusAngle, double focusDist,
+ *                                 float[] outCamera);   // returns the defocus flag
  *   static native int deviceCount();
+ *   static native int writePpm(String path, byte[] rgb, int width, int height);
  *   static native int writePng(String path, byte[] rgb, int width, int height);
  *   static native int ppmToPng(String srcPpm, String dstPng);
  * camera = 18 floats: center, p00, du, dv, disk_u, disk_v (rt_camera order).
- * Replaces compute-pixel + the executor (src/raytracing.clj:141-171) and
- * ppm2png/ppm->png (src/ppm2png.clj:35-87).
+ * Replaces compute-pixel + the executor (src/raytracing.clj:141-171), the
+ * camera let block (:105-139), write-color! and the PPM writer (:19-26,
+ * :172-175) and ppm2png/ppm->png (src/ppm2png.clj:35-87).
  */
 #include <jni.h>
 #include <stdio.h>
@@ -39,9 +47,10 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_deviceCount(JNIEnv* env, jclass cls) {
   return rt_device_count();
 }
 
+/* out_rgb: a float[] (rt_render) or, u8, a byte[] (rt_render_u8) */
 static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloatArray mats, jfloatArray camera,
                         jint defocus, jint width, jint height, jint spp, jint depth, jlong seed, jint n_gpus,
-                        jint flags, jfloatArray out_rgb) {
+                        jint flags, jarray out_rgb, int u8) {
   if (!spheres || !kinds || !mats || !camera || !out_rgb) { /* Java nulls */
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
@@ -53,7 +62,7 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
   }
-  /* The frame is width x height x 3 floats; a longer Java array keeps its
+  /* The frame is width x height x 3 floats (bytes); a longer Java array keeps its
    * tail (only the frame is copied back), a shorter one is an argument error
    * raised before anything is rendered. */
   if (width <= 0 || height <= 0 || (*env)->GetArrayLength(env, out_rgb) / 3 / width < height) {
@@ -62,14 +71,14 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   }
   const size_t frame = (size_t)width * (size_t)height * 3;
   /* Copy every input; render into a malloc'd buffer and copy the frame back
-   * with SetFloatArrayRegion.  Nothing is pinned while rt_render runs (a full
+   * with Set<Float|Byte>ArrayRegion.  Nothing is pinned while rt_render runs (a full
    * multi-GPU frame can take seconds: a critical section would block GC
    * JVM-wide for that long).  A failed copy leaves an OutOfMemoryError
    * pending: no further JNI call but the releases is made after it. */
   float* sph = NULL;
   jint* knd = NULL;
   float* mat = NULL;
-  float* out = NULL;
+  void* out = NULL;
   float cam18[18];
   int rc = RT_E_ARG;
   if (!(sph = (float*)(*env)->GetFloatArrayElements(env, spheres, NULL))) goto done;
@@ -77,7 +86,7 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   if (!(mat = (float*)(*env)->GetFloatArrayElements(env, mats, NULL))) goto done;
   (*env)->GetFloatArrayRegion(env, camera, 0, 18, cam18);
   if ((*env)->ExceptionCheck(env)) goto done;
-  if (!(out = (float*)malloc(frame * sizeof(float)))) {
+  if (!(out = malloc(frame * (u8 ? 1 : sizeof(float))))) {
     /* out of memory, not a bad argument: java.lang.OutOfMemoryError */
     jclass oom = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
     if (oom) (*env)->ThrowNew(env, oom, "rtclj render: cannot allocate the frame buffer");
@@ -104,8 +113,13 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   p.seed = (uint64_t)seed;
   p.n_devices = n_gpus;
   p.flags = flags;
-  rc = rt_render(&scene, &cam, &p, out, frame, NULL);
-  if (rc >= 0) (*env)->SetFloatArrayRegion(env, out_rgb, 0, (jsize)frame, out);
+  if (u8) {
+    rc = rt_render_u8(&scene, &cam, &p, (uint8_t*)out, frame, NULL);
+    if (rc >= 0) (*env)->SetByteArrayRegion(env, out_rgb, 0, (jsize)frame, (const jbyte*)out);
+  } else {
+    rc = rt_render(&scene, &cam, &p, (float*)out, frame, NULL);
+    if (rc >= 0) (*env)->SetFloatArrayRegion(env, out_rgb, 0, (jsize)frame, (const jfloat*)out);
+  }
 done:
   free(out);
   if (sph) (*env)->ReleaseFloatArrayElements(env, spheres, (jfloat*)sph, JNI_ABORT);
@@ -121,7 +135,7 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_render(JNIEnv* env, jclass cls, jfloatA
                                                 jfloatArray out_rgb) {
   (void)cls;
   return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, 0,
-                     out_rgb);
+                     out_rgb, 0);
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls, jfloatArray spheres,
@@ -131,7 +145,72 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls
                                                          jfloatArray out_rgb) {
   (void)cls;
   return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, flags,
-                     out_rgb);
+                     out_rgb, 0);
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_renderBytes(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
+                                                     jfloatArray mats, jfloatArray camera, jint defocus, jint width,
+                                                     jint height, jint spp, jint depth, jlong seed, jint n_gpus,
+                                                     jint flags, jbyteArray out_rgb) {
+  (void)cls;
+  return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, flags,
+                     out_rgb, 1);
+}
+
+/* -main's camera let block (raytracing.clj:105-139) through rt_camera_setup:
+ * out_camera (>= 18 floats) gets the rt_camera order; returns the defocus
+ * flag (0/1) or a negative status. */
+JNIEXPORT jint JNICALL Java_rtclj_Native_cameraSetup(JNIEnv* env, jclass cls, jint width, jint height, jdouble vfov,
+                                                     jdoubleArray look_from, jdoubleArray look_at, jdoubleArray vup,
+                                                     jdouble defocus_angle, jdouble focus_dist,
+                                                     jfloatArray out_camera) {
+  (void)cls;
+  if (!look_from || !look_at || !vup || !out_camera || (*env)->GetArrayLength(env, look_from) != 3 ||
+      (*env)->GetArrayLength(env, look_at) != 3 || (*env)->GetArrayLength(env, vup) != 3 ||
+      (*env)->GetArrayLength(env, out_camera) < 18) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
+  double lf[3], la[3], up[3];
+  (*env)->GetDoubleArrayRegion(env, look_from, 0, 3, lf);
+  if (!(*env)->ExceptionCheck(env)) (*env)->GetDoubleArrayRegion(env, look_at, 0, 3, la);
+  if (!(*env)->ExceptionCheck(env)) (*env)->GetDoubleArrayRegion(env, vup, 0, 3, up);
+  if ((*env)->ExceptionCheck(env)) return RT_E_ARG;
+  rt_camera cam;
+  const int rc = rt_camera_setup(width, height, vfov, lf, la, up, defocus_angle, focus_dist, &cam);
+  if (rc < 0) {
+    throw_rt(env, rc);
+    return rc;
+  }
+  float out[18];
+  memcpy(out + 0, cam.center, 12);
+  memcpy(out + 3, cam.p00, 12);
+  memcpy(out + 6, cam.du, 12);
+  memcpy(out + 9, cam.dv, 12);
+  memcpy(out + 12, cam.disk_u, 12);
+  memcpy(out + 15, cam.disk_v, 12);
+  (*env)->SetFloatArrayRegion(env, out_camera, 0, 18, out);
+  return (*env)->ExceptionCheck(env) ? RT_E_ARG : cam.defocus;
+}
+
+/* The PPM writer of -main (raytracing.clj:172-175) through rt_write_ppm. */
+JNIEXPORT jint JNICALL Java_rtclj_Native_writePpm(JNIEnv* env, jclass cls, jstring path, jbyteArray rgb, jint width,
+                                                  jint height) {
+  (void)cls;
+  if (!path || !rgb || width <= 0 || height <= 0 ||
+      (jlong)(*env)->GetArrayLength(env, rgb) < (jlong)width * height * 3) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
+  int rc = RT_E_ARG;
+  jbyte* px = NULL;
+  const char* p = (*env)->GetStringUTFChars(env, path, NULL);
+  if (p && (px = (*env)->GetByteArrayElements(env, rgb, NULL)) != NULL)
+    rc = rt_write_ppm(p, (const uint8_t*)px, width, height);
+  if (px) (*env)->ReleaseByteArrayElements(env, rgb, px, JNI_ABORT);
+  if (p) (*env)->ReleaseStringUTFChars(env, path, p);
+  if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_rt(env, rc);
+  return rc;
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_writePng(JNIEnv* env, jclass cls, jstring path, jbyteArray rgb, jint width,

@@ -46,6 +46,36 @@
                             (if realm? Native/FLAG_REALM 0) out)
     out))
 
+(defn render-bytes
+  "render, then write-color! on the device (rt_render_u8): width*height*3
+  bytes, the 0..255 values -main writes (raytracing.clj:19-26)."
+  [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
+   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
+  (let [[sph knd mat] (flatten-bodies bodies)
+        cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))
+        out (byte-array (* width height 3))]
+    (Native/renderBytes sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
+                        samples-per-px max-depth (long seed) (int gpus)
+                        (if realm? Native/FLAG_REALM 0) out)
+    out))
+
+(defn camera
+  "-main's camera values (raytracing.clj:105-139) through rt_camera_setup, in
+  the keys render takes."
+  [width height {:keys [vfov look-from look-at vup defocus-angle focus-dist]}]
+  (let [out (float-array 18)
+        _ (Native/cameraSetup (int width) (int height) (double vfov) (double-array look-from)
+                              (double-array look-at) (double-array vup) (double defocus-angle)
+                              (double focus-dist) out)
+        v (fn [i] (vec (take 3 (drop i out))))]
+    {:center (v 0) :pixel-00-loc (v 3) :pixel-du (v 6) :pixel-dv (v 9)
+     :defocus-disk-u (v 12) :defocus-disk-v (v 15) :defocus-angle defocus-angle}))
+
+(defn write-ppm!
+  "rgb: width*height*3 bytes -> the P3 file -main writes (raytracing.clj:172-175)."
+  [path ^bytes rgb width height]
+  (Native/writePpm (str path) rgb (int width) (int height)))
+
 (defn write-png!
   "rgb: width*height*3 bytes (write-color!'s 0..255 values) -> PNG file."
   [path ^bytes rgb width height]
@@ -55,3 +85,26 @@
   "src/ppm2png.clj:35-87's ppm->png through the library."
   [source dest]
   (Native/ppmToPng (str source) (str dest)))
+
+;; The reference's five bodies (raytracing.clj:63-78) as data.
+(def hittables
+  [{:center [0.0 -100.5 -1.0] :radius 100.0 :material {:type :lambertian :albedo [0.8 0.8 0.0]}}
+   {:center [0.0 0.0 -1.2] :radius 0.5 :material {:type :lambertian :albedo [0.1 0.2 0.5]}}
+   {:center [-1.0 0.0 -1.0] :radius 0.5 :material {:type :dielectric :refraction-index 1.5}}
+   {:center [-1.0 0.0 -1.0] :radius 0.4 :material {:type :dielectric :refraction-index (/ 1.0 1.5)}}
+   {:center [1.0 0.0 -1.0] :radius 0.5 :material {:type :metal :albedo [0.8 0.6 0.2] :fuzz 1.0}}])
+
+(defn -main
+  "`clojure -M:main [spp] [depth]` (raytracing.clj:95-177) on the GPU: the
+  same config line, (time ...) around render + PPM, scene.ppm."
+  [& args]
+  (let [spp (if (first args) (Integer/parseInt (first args)) 100)
+        depth (if (second args) (Integer/parseInt (second args)) 50)
+        width 400
+        height (int (/ width 16/9))]
+    (println "config:" {:samples-per-px spp :max-depth depth})
+    (time
+     (let [cam (camera width height {:vfov 20.0 :look-from [-2.0 2.0 1.0] :look-at [0.0 0.0 -1.0]
+                                     :vup [0.0 1.0 0.0] :defocus-angle 10.0 :focus-dist 3.4})
+           rgb (render-bytes hittables cam {:width width :height height :samples-per-px spp :max-depth depth})]
+       (write-ppm! "scene.ppm" rgb width height)))))

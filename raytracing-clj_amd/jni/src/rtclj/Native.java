@@ -20,6 +20,18 @@ public final class Native {
 
   public static final int FLAG_REALM = 2;
 
+  /** render + write-color! on the device (rt_render_u8): rows x width x 3 bytes. */
+  public static native int renderBytes(float[] spheres, int[] kinds, float[] mats, float[] camera, int defocus,
+                                       int width, int height, int spp, int depth, long seed, int nGpus, int flags,
+                                       byte[] outRgb);
+
+  /** -main's camera values (rt_camera_setup) into outCamera[18]; returns the defocus flag. */
+  public static native int cameraSetup(int width, int height, double vfov, double[] lookFrom, double[] lookAt,
+                                       double[] vup, double defocusAngle, double focusDist, float[] outCamera);
+
+  /** The P3 file of -main (rt_write_ppm). */
+  public static native int writePpm(String path, byte[] rgb, int width, int height);
+
   public static native int deviceCount();
 
   /** 8-bit RGB PNG of width x height x 3 bytes (rt_write_png). */

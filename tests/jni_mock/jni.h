@@ -26,6 +26,7 @@ typedef int64_t jlong;
 typedef int8_t jbyte;
 typedef uint8_t jboolean;
 typedef float jfloat;
+typedef double jdouble;
 typedef jint jsize;
 
 typedef struct mock_obj* jobject;
@@ -36,6 +37,7 @@ typedef jobject jthrowable;
 typedef jarray jfloatArray;
 typedef jarray jintArray;
 typedef jarray jbyteArray;
+typedef jarray jdoubleArray;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -53,6 +55,8 @@ struct JNINativeInterface_ {
   void (*ReleaseByteArrayElements)(JNIEnv* env, jbyteArray a, jbyte* elems, jint mode);
   void (*GetFloatArrayRegion)(JNIEnv* env, jfloatArray a, jsize start, jsize len, jfloat* buf);
   void (*SetFloatArrayRegion)(JNIEnv* env, jfloatArray a, jsize start, jsize len, const jfloat* buf);
+  void (*SetByteArrayRegion)(JNIEnv* env, jbyteArray a, jsize start, jsize len, const jbyte* buf);
+  void (*GetDoubleArrayRegion)(JNIEnv* env, jdoubleArray a, jsize start, jsize len, jdouble* buf);
   const char* (*GetStringUTFChars)(JNIEnv* env, jstring s, jboolean* is_copy);
   void (*ReleaseStringUTFChars)(JNIEnv* env, jstring s, const char* chars);
 };

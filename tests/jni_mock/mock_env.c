@@ -7,7 +7,7 @@
  *     the pointer it returned (inputs: mode JNI_ABORT, nothing written back);
  *   - no JNI call other than ExceptionCheck and the releases while an
  *     exception is pending;
- *   - Get/SetFloatArrayRegion within the array's bounds.
+ *   - Get/Set<Type>ArrayRegion within the array's bounds.
  * mock_fail_get(k) makes the k-th following Get*Elements return NULL with a
  * pending OutOfMemoryError, as a JVM does when it cannot copy an array.
  */
@@ -17,7 +17,7 @@
 
 #include "jni.h"
 
-enum { T_FLOAT = 1, T_INT, T_BYTE, T_STRING, T_CLASS };
+enum { T_FLOAT = 1, T_INT, T_BYTE, T_STRING, T_CLASS, T_DOUBLE };
 
 struct mock_obj {
   int type;
@@ -58,7 +58,7 @@ static struct mock_obj* new_obj(int type, jsize len, size_t esz, const void* src
   return o;
 }
 
-static size_t esize(int type) { return type == T_BYTE ? 1 : 4; }
+static size_t esize(int type) { return type == T_BYTE ? 1 : type == T_DOUBLE ? 8 : 4; }
 
 static int fail_now(void) {
   if (st.fail_get_in <= 0) return 0;
@@ -170,6 +170,29 @@ static void m_SetFloatArrayRegion(JNIEnv* env, jfloatArray a, jsize start, jsize
   }
   memcpy((float*)a->data + start, buf, (size_t)len * 4);
 }
+static void m_SetByteArrayRegion(JNIEnv* env, jbyteArray a, jsize start, jsize len, const jbyte* buf) {
+  (void)env;
+  record_call();
+  st.set_regions++;
+  if (!a || a->type != T_BYTE || start < 0 || len < 0 || start + len > a->len) {
+    st.region_oob++;
+    st.pending = 1;
+    snprintf(st.cls, sizeof st.cls, "java/lang/ArrayIndexOutOfBoundsException");
+    return;
+  }
+  memcpy((jbyte*)a->data + start, buf, (size_t)len);
+}
+static void m_GetDoubleArrayRegion(JNIEnv* env, jdoubleArray a, jsize start, jsize len, jdouble* buf) {
+  (void)env;
+  record_call();
+  if (!a || a->type != T_DOUBLE || start < 0 || len < 0 || start + len > a->len) {
+    st.region_oob++;
+    st.pending = 1;
+    snprintf(st.cls, sizeof st.cls, "java/lang/ArrayIndexOutOfBoundsException");
+    return;
+  }
+  memcpy(buf, (double*)a->data + start, (size_t)len * 8);
+}
 static const char* m_GetStringUTFChars(JNIEnv* env, jstring s, jboolean* c) {
   (void)env;
   if (c) *c = JNI_TRUE;
@@ -202,6 +225,7 @@ static const struct JNINativeInterface_ table = {
     m_GetIntArrayElements, m_ReleaseIntArrayElements,
     m_GetByteArrayElements, m_ReleaseByteArrayElements,
     m_GetFloatArrayRegion, m_SetFloatArrayRegion,
+    m_SetByteArrayRegion,  m_GetDoubleArrayRegion,
     m_GetStringUTFChars,   m_ReleaseStringUTFChars,
 };
 static JNIEnv the_env = &table;
@@ -222,13 +246,14 @@ JNIEXPORT void mock_reset(void) {
 JNIEXPORT jobject mock_float_array(const float* src, jsize len) { return new_obj(T_FLOAT, len, 4, src); }
 JNIEXPORT jobject mock_int_array(const int32_t* src, jsize len) { return new_obj(T_INT, len, 4, src); }
 JNIEXPORT jobject mock_byte_array(const int8_t* src, jsize len) { return new_obj(T_BYTE, len, 1, src); }
+JNIEXPORT jobject mock_double_array(const double* src, jsize len) { return new_obj(T_DOUBLE, len, 8, src); }
 JNIEXPORT jobject mock_string(const char* s) { return new_obj(T_STRING, (jsize)strlen(s), 1, s); }
 JNIEXPORT void* mock_data(jobject o) { return o ? o->data : NULL; }
 JNIEXPORT void mock_fail_get(int k) { st.fail_get_in = k; }
 
 /* out[8]: pins outstanding (gets - releases over every object), bad releases,
  * calls while an exception was pending, throws, out-of-bounds regions,
- * SetFloatArrayRegion calls, exception pending, total gets. */
+ * Set<Float|Byte>ArrayRegion calls, exception pending, total gets. */
 JNIEXPORT void mock_stats(int* out) {
   int outstanding = 0, gets = 0;
   for (int i = 0; i < n_objs; ++i) {

@@ -13,7 +13,9 @@ JDK in this image).  A logic test of the shim, not JVM verification:
   * the rt error -> exception mapping (rt_render's code and rt_last_error());
   * on the GPU box: the shim's render equals rt_render's pixels bit for bit
     (both flags), and only the frame is copied back (a longer Java array keeps
-    its tail: ADVICE r02).
+    its tail: ADVICE r02); renderBytes equals rt_render_u8's bytes;
+  * cameraSetup equals rt_camera_setup (-main's camera let block,
+    raytracing.clj:105-139); writePpm writes what rt_write_ppm writes.
 
 Replaces compute-pixel + the executor (src/raytracing.clj:141-171) and
 ppm->png (src/ppm2png.clj:35-87) for a Clojure host.
@@ -43,6 +45,8 @@ def _load():
     for f in ("mock_float_array", "mock_int_array", "mock_byte_array"):
         getattr(d, f).restype = VP
         getattr(d, f).argtypes = [VP, C.c_int32]
+    d.mock_double_array.restype = VP
+    d.mock_double_array.argtypes = [VP, C.c_int32]
     d.mock_string.restype = VP
     d.mock_string.argtypes = [C.c_char_p]
     d.mock_data.restype = VP
@@ -57,6 +61,12 @@ def _load():
     d.Java_rtclj_Native_renderWithFlags.restype = i32
     d.Java_rtclj_Native_renderWithFlags.argtypes = [VP, VP, VP, VP, VP, VP, i32, i32, i32, i32, i32, i64, i32, i32,
                                                      VP]
+    d.Java_rtclj_Native_renderBytes.restype = i32
+    d.Java_rtclj_Native_renderBytes.argtypes = [VP, VP, VP, VP, VP, VP, i32, i32, i32, i32, i32, i64, i32, i32, VP]
+    d.Java_rtclj_Native_cameraSetup.restype = i32
+    d.Java_rtclj_Native_cameraSetup.argtypes = [VP, VP, i32, i32, C.c_double, VP, VP, VP, C.c_double, C.c_double, VP]
+    d.Java_rtclj_Native_writePpm.restype = i32
+    d.Java_rtclj_Native_writePpm.argtypes = [VP, VP, VP, VP, i32, i32]
     d.Java_rtclj_Native_deviceCount.restype = i32
     d.Java_rtclj_Native_deviceCount.argtypes = [VP, VP]
     d.Java_rtclj_Native_writePng.restype = i32
@@ -101,6 +111,20 @@ def iarr(d, a):
 
 def read_f(d, obj, n):
     return np.ctypeslib.as_array(C.cast(d.mock_data(obj), C.POINTER(C.c_float)), (n,)).copy()
+
+
+def read_b(d, obj, n):
+    return np.ctypeslib.as_array(C.cast(d.mock_data(obj), C.POINTER(C.c_uint8)), (n,)).copy()
+
+
+def barr(d, a):
+    a = np.ascontiguousarray(a, np.uint8).view(np.int8)
+    return d.mock_byte_array(a.ctypes.data, a.size)
+
+
+def darr(d, a):
+    a = np.ascontiguousarray(a, np.float64)
+    return d.mock_double_array(a.ctypes.data, a.size)
 
 
 def _scene_args(d):
@@ -186,6 +210,74 @@ def test_rt_error_maps_to_runtime_exception(jni):
     assert np.all(read_f(d, out, w * h * 3) == 7.0)
 
 
+def test_render_bytes_checks_and_errors(jni):
+    """renderBytes: a byte[] shorter than the frame is an argument error
+    before any copy; a well-formed call maps rt_render_u8's status (no GPU
+    here: RT_E_NODEV) and leaves the Java array untouched."""
+    import rtclj
+    d = jni
+    env = d.mock_env()
+    sc, cam, w, h, (sph, knd, mat, c18) = _scene_args(d)
+    short = barr(d, np.full(w * h * 3 - 1, 9))
+    rc = d.Java_rtclj_Native_renderBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 4, 50, 1, 1, 0, short)
+    st = stats(d)
+    assert rc == RT_E_ARG and st["pending"] and clean(st) and st["gets"] == 0, st
+    d.mock_clear_exception()
+    out = barr(d, np.full(w * h * 3, 9))
+    rc = d.Java_rtclj_Native_renderBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 4, 50, 1, 1, 0, out)
+    st = stats(d)
+    assert clean(st) and st["gets"] == 3, st
+    if rtclj.lib.rt_device_count() > 0:
+        assert rc == 0 and st["set_regions"] == 1
+        return
+    assert rc == RT_E_NODEV and st["pending"] and st["set_regions"] == 0
+    assert np.all(read_b(d, out, w * h * 3) == 9)
+
+
+def test_camera_setup_equals_rt_camera_setup(jni):
+    from rtclj import raytracing as R
+    d = jni
+    env = d.mock_env()
+    rc_cam = R.REFERENCE_CAMERA
+    out = farr(d, np.zeros(18))
+    rc = d.Java_rtclj_Native_cameraSetup(env, None, 400, 225, float(rc_cam["vfov"]), darr(d, rc_cam["look_from"]),
+                                         darr(d, rc_cam["look_at"]), darr(d, rc_cam["vup"]),
+                                         float(rc_cam["defocus_angle"]), float(rc_cam["focus_dist"]), out)
+    st = stats(d)
+    ref = R.camera(400, 225, **rc_cam)
+    assert rc == ref.defocus == 1 and clean(st) and not st["pending"] and st["set_regions"] == 1, st
+    assert np.array_equal(read_f(d, out, 18), np.asarray(ref.as_list(), np.float32))
+    # wrong lengths, a null, a bad image size (rt_camera_setup's own check)
+    for args in ((darr(d, [0, 0]), darr(d, [0, 0, 0]), darr(d, [0, 1, 0]), out),
+                 (darr(d, [0, 0, 1]), None, darr(d, [0, 1, 0]), out),
+                 (darr(d, [0, 0, 1]), darr(d, [0, 0, 0]), darr(d, [0, 1, 0]), farr(d, np.zeros(17)))):
+        d.mock_clear_exception()
+        rc = d.Java_rtclj_Native_cameraSetup(env, None, 400, 225, 20.0, *args[:3], 0.0, 1.0, args[3])
+        assert rc == RT_E_ARG and d.mock_exception_class() == b"java/lang/RuntimeException"
+    d.mock_clear_exception()
+    rc = d.Java_rtclj_Native_cameraSetup(env, None, 0, 225, 20.0, darr(d, [0, 0, 1]), darr(d, [0, 0, 0]),
+                                         darr(d, [0, 1, 0]), 0.0, 1.0, out)
+    assert rc == RT_E_ARG and clean(stats(d))
+
+
+def test_write_ppm_equals_rt_write_ppm(jni, tmp_path):
+    from rtclj import raytracing as R
+    d = jni
+    env = d.mock_env()
+    px = np.random.default_rng(5).integers(0, 256, size=(6, 9, 3), dtype=np.uint8)
+    rgb = barr(d, px.reshape(-1))
+    rc = d.Java_rtclj_Native_writePpm(env, None, d.mock_string(str(tmp_path / "a.ppm").encode()), rgb, 9, 6)
+    st = stats(d)
+    assert rc == 0 and clean(st) and not st["pending"], st
+    R.write_ppm(tmp_path / "b.ppm", px)
+    assert (tmp_path / "a.ppm").read_bytes() == (tmp_path / "b.ppm").read_bytes()
+    rc = d.Java_rtclj_Native_writePpm(env, None, d.mock_string(str(tmp_path / "a.ppm").encode()), rgb, 9, 7)
+    assert rc == RT_E_ARG and d.mock_exception_message().startswith(b"rt error -1: ")
+    d.mock_clear_exception()
+    rc = d.Java_rtclj_Native_writePpm(env, None, d.mock_string(str(tmp_path / "no" / "a.ppm").encode()), rgb, 9, 6)
+    assert rc == RT_E_IO and clean(stats(d))
+
+
 def test_device_count_matches_the_library(jni):
     import rtclj
     assert jni.Java_rtclj_Native_deviceCount(jni.mock_env(), None) == rtclj.lib.rt_device_count()
@@ -250,3 +342,13 @@ def test_shim_render_equals_rt_render(gpu_lib, jni):
         ref = R.render(sc, cam, w, h, spp=8, max_depth=50, seed=3, flags=flags or 0)
         assert np.array_equal(got[:n].reshape(h, w, 3), ref)
         assert np.all(got[n:] == 7.0)
+        # renderBytes: rt_render_u8's bytes == write-color! of those pixels
+        ob = barr(d, np.full(n + 3, 9))
+        sph, knd, mat, c18 = arrays
+        rc = d.Java_rtclj_Native_renderBytes(d.mock_env(), None, sph, knd, mat, c18, cam.defocus, w, h, 8, 50, 3, 1,
+                                             flags or 0, ob)
+        st = stats(d)
+        assert rc == 0 and clean(st) and not st["pending"], st
+        gb = read_b(d, ob, n + 3)
+        assert np.array_equal(gb[:n].reshape(h, w, 3), R.write_color(ref))
+        assert np.all(gb[n:] == 9)
