@@ -312,16 +312,18 @@ PARTS = ("upload_ms", "setup_ms", "enqueue_ms", "wait_ms", "scatter_ms", "other_
 
 def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
     """rt_render, the product entry point the JNI shim calls: the scene cache
-    (the first call uploads and builds the BVHs), the N-device fan-out with
-    one host thread per device, D2H and the host gather into one caller
-    buffer.  The first call of the process (rt_cache_clear() first, so it
+    (the first call uploads and builds the BVHs), the N-device fan-out (a
+    task per device on the library's host worker pool), D2H straight into
+    the rows of one caller buffer.  The first call of the process (rt_cache_clear() first, so it
     pays the scene upload, the BVH builds and the device context set-up, as
     the reference's one-frame `-main` does), `warm` untimed calls (the
     adaptive tile order converges over ~3 launches: tools/e2e_calls.py), then
     `reps` timed calls into one reused framebuffer, as a renderer drawing
     frames runs, whose median is the value (min and max beside it).  `parts`
     are rt_stats' host clocks of the slowest device's share; they add up to
-    total_ms."""
+    total_ms.  `bytes`: the same calls through rt_render_u8 (write-color! on
+    the device, a quarter of the copy back), checked equal to rt_quantize of
+    the float frame."""
     import numpy as np
     visible = lib.rt_device_count()
     flags = RT_FLAG_SHARDS_ON_DEVICE0 if n_dev > visible else 0
@@ -341,6 +343,17 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
         runs.append(st)
     runs.sort(key=lambda r: r["total_ms"])
     med = runs[len(runs) // 2]
+    # rt_render_u8: the frame as write-color!'s bytes (the PPM's), quantised on the device
+    b8 = None
+    u8_runs = []
+    for i in range(warm + reps):
+        st = {}
+        b8 = R.render(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, stats=st, out=b8, u8=True)
+        if i >= warm:
+            u8_runs.append(st)
+    u8_runs.sort(key=lambda r: r["total_ms"])
+    u8_med = u8_runs[len(u8_runs) // 2]
+    u8_equal = bool(np.array_equal(b8, R.write_color(out)))
 
     def parts(r):
         return {k: r[k] for k in PARTS}
@@ -359,6 +372,10 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
                                    "(upload_ms), the device context (setup_ms: stream, events, framebuffer, pinned "
                                    "counters), the launch enqueue (enqueue_ms; the first launch of a kernel loads "
                                    "its code object), the device work (wait_ms: kernel in plain tile order + D2H)"},
+            "bytes": {"entry": "rt_render_u8 (include/rt.h)", "statistic": f"median of {reps} calls",
+                      "total_ms": u8_med["total_ms"], "kernel_ms_max": u8_med["kernel_ms"],
+                      "d2h_ms": u8_med["d2h_ms"], "equals_rt_quantize_of_rt_render": u8_equal,
+                      "note": "d2h_ms includes the quantise kernel"},
             "repeats": reps, "warm_calls": warm}, out
 
 
