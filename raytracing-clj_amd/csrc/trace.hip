@@ -189,20 +189,28 @@ __device__ __forceinline__ void wave_event(uint64_t& c) {
 
 // vec3a/random-unit-vec3 (vec3a.clj:74-79): rejection in [-1,1)^3 with
 // 0 < |v|^2 <= 1 (1e-160 underflows to 0 in fp32), then v / |v|.
+// (A software-pipelined form -- the next trip's states made while this
+// trip's |v|^2 is tested -- measured 1.9 % slower on C1: the speculative
+// trip's VALU costs more than the overlap saves; profiles/r04/kernel_b/.)
 template <bool STATS = false>
 __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, float& z, uint64_t* trips = nullptr,
                                             uint64_t* flops = nullptr) {
   float l2;
+  // (the trip loop tests only |v|^2 <= 1, one compare a trip; v = 0, which
+  // needs three draws of exactly 2^23, is sent back to the loop after it)
   do {
-    if constexpr (STATS) {
-      wave_event(*trips);
-      *flops += 11;   // 3 x (2 xi - 1) + |v|^2
-    }
-    x = rng_sym(s);
-    y = rng_sym(s);
-    z = rng_sym(s);
-    l2 = fmaf(z, z, fmaf(y, y, x * x));
-  } while (!(l2 > 0.0f && l2 <= 1.0f));
+    do {
+      if constexpr (STATS) {
+        wave_event(*trips);
+        *flops += 11;   // 3 x (2 xi - 1) + |v|^2
+      }
+      x = rng_sym(s);
+      y = rng_sym(s);
+      z = rng_sym(s);
+      l2 = fmaf(z, z, fmaf(y, y, x * x));
+    } while (!(l2 <= 1.0f));
+    asm volatile("" : "+v"(l2));   // (keeps the two loops apart: one test a trip)
+  } while (__builtin_expect(!(l2 > 0.0f), 0));
   const float il = 1.0f / sqrt_rn(l2);   // contract: v * (1/|v|)
   if constexpr (STATS) *flops += 5;
   x = x * il;
@@ -308,6 +316,11 @@ constexpr int leaf_pairs(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
+// LDS (address space 3) pointers: 32-bit addresses, ds_read with immediate offsets
+typedef const char __attribute__((address_space(3)))* LdsC;
+typedef const f2 __attribute__((address_space(3)))* LdsF2;
+typedef const long long __attribute__((address_space(3)))* LdsI64;
+__device__ __forceinline__ unsigned lds_addr(const void* p) { return static_cast<unsigned>((uintptr_t)(LdsC)p); }
 struct alignas(16) Pair {
   f2 x, y, z, w;   // centres and -r^2 of bodies 2p and 2p+1
 };
@@ -329,6 +342,8 @@ static_assert(sizeof(KNode) == 80, "KNode layout");
 // traversal, whose large-scene LDS image (C4: 1000 bodies) needs the 768 B
 // that half the pixel sums give back to stay at 5 workgroups per CU
 constexpr int kTile = 8;
+// the 4-body tree's leaf record in LDS: two pairs and their index pairs
+constexpr int kLeafRecBytes = 80;
 constexpr int kPoolPx = kTile * kTile;
 constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_BVHS ? 16 : kTile; }
 
@@ -455,7 +470,38 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   }
   // the scene image (a thief only once it has samples to run)
   if constexpr (SRC == SRC_LDS) {
-    if constexpr (is_bvh_scan(SCAN)) {
+    if constexpr (SCAN == SCAN_BVHQ) {
+      // the 4-body tree's inner-child refs (node byte offsets in the blob)
+      // become LDS addresses as they are copied: a node step then reads its
+      // child refs at ref + 72 and its planes at ref + the ray's plane
+      // offsets, with no base added (float4 4 of each 80-byte node holds
+      // c0, c1 in .z, .w; leaf refs are negative and stay)
+      // The leaves are laid out as records: a leaf's two pairs (64 B) and
+      // their body indices (16 B) side by side, 80 B, so a leaf pass reads
+      // everything from one address; a leaf ref ~p (p = its first pair, even)
+      // becomes ~(the record's LDS address).
+      const int nb0 = static_cast<int>(lds_addr(s_geo));
+      const int nodes_f4 = a.bvh_off_pairs >> 4;
+      const int pairs_f4 = (a.bvh_off_pidx - a.bvh_off_pairs) >> 4;   // 2 per pair
+      const int rec0 = nb0 + (nodes_f4 << 4);
+      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) {
+        float4 v = a.bvh_blob[i];
+        int d = i;
+        if (i < nodes_f4) {
+          if (i % 5 == 4) {
+            const int r0 = __float_as_int(v.z), r1 = __float_as_int(v.w);
+            v.z = __int_as_float(r0 >= 0 ? r0 + nb0 : ~(rec0 + (~r0 >> 1) * kLeafRecBytes));
+            v.w = __int_as_float(r1 >= 0 ? r1 + nb0 : ~(rec0 + (~r1 >> 1) * kLeafRecBytes));
+          }
+        } else if (i < nodes_f4 + pairs_f4) {   // pair k / 2, half k % 2
+          const int k = i - nodes_f4, pr = k >> 1;
+          d = nodes_f4 + (pr >> 1) * 5 + (pr & 1) * 2 + (k & 1);
+        } else {                                 // the indices of pairs 2k, 2k + 1
+          d = nodes_f4 + (i - nodes_f4 - pairs_f4) * 5 + 4;
+        }
+        s_geo[d] = v;
+      }
+    } else if constexpr (is_bvh_scan(SCAN)) {
       for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
     } else {
       const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
@@ -1043,9 +1089,14 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       f2 nf_z = {sz ? nhz : nlz, sz ? nlz : nhz};
       // byte offsets of the (near, far) pairs of each axis inside a node
       const int offx = sx ? 8 : 0, offy = 24 + (sy ? 8 : 0), offz = 48 + (sz ? 8 : 0);
+      // the ray's (near, far) plane pairs of node 0; opaque, so that a node's
+      // three axis addresses are one add each from them (not the blob's base
+      // added to the node first)
       f2 o_xy = {ox, oy}, o_zux = {oz, ux}, u_yz = {uy, uz};
       // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
       // size 4), tested packed; the acceptance is order-independent
+      // (the 4-body tree in LDS: p is a leaf record's LDS address, see the copy)
+      constexpr bool kLeafRec = SRC == SRC_LDS && SCAN == SCAN_BVHQ;
       auto leaf = [&](int p) {
         if constexpr (STATS) {
           ++st_blk;
@@ -1066,11 +1117,26 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         // rest; indexing p + 1 let the compiler rebuild it as -c, a 2nd base)
         const Pair* const lp = pairs + p;
         const PidxT* const li = pidx + p;
+        // (a leaf record's address opaque: its reads are immediate offsets
+        // from it, not (k - 1) - c rebuilt from the ref c = ~address per read)
+        unsigned pa = static_cast<unsigned>(p);
+        if constexpr (kLeafRec) asm volatile("" : "+v"(pa));
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
           if constexpr (STATS) st_fl += 32;   // 2 bodies x (oc 3, h 5, c 6, disc 2)
-          const Pair g = lp[hb + q];
-          const PidxT id = li[hb + q];
+          Pair g;
+          PidxT id;
+          if constexpr (kLeafRec) {
+            // p is the leaf record's LDS address: pair q at + 32 q, its
+            // indices at + 64 + 8 q (immediate offsets of one address)
+            const LdsF2 lg = (LdsF2)(uintptr_t)(pa + 32u * (hb + q));
+            g.x = lg[0], g.y = lg[1], g.z = lg[2], g.w = lg[3];
+            const long long i2 = *(LdsI64)(uintptr_t)(pa + 64u + 8u * (hb + q));
+            id = PidxT{static_cast<int>(i2), static_cast<int>(i2 >> 32)};
+          } else {
+            g = lp[hb + q];
+            id = li[hb + q];
+          }
           asm volatile("" : "+v"(o_xy), "+v"(o_zux), "+v"(u_yz));
           const f2 ocx = g.x - bc_lo(o_xy), ocy = g.y - bc_hi(o_xy), ocz = g.z - bc_lo(o_zux);
           const f2 h = fma2(bc_hi(u_yz), ocz, fma2(bc_lo(u_yz), ocy, bc_hi(o_zux) * ocx));
@@ -1138,35 +1204,55 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
         // the 4-body tree's inner-child refs are byte offsets (node * 80,
         // written by rt_scene_upload): no multiply per step
-        const char* nb = reinterpret_cast<const char*>(nodes) +
-                         (SCAN == SCAN_BVHQ ? static_cast<unsigned>(node) : __umul24(static_cast<unsigned>(node), 80u));
-        const f2* ax = reinterpret_cast<const f2*>(nb + offx);
-        const f2* ay = reinterpret_cast<const f2*>(nb + offy);
-        const f2* az = reinterpret_cast<const f2*>(nb + offz);
-        const int2 ch = *reinterpret_cast<const int2*>(nb + 72);
+        const unsigned nof = SCAN == SCAN_BVHQ ? static_cast<unsigned>(node) : __umul24(static_cast<unsigned>(node), 80u);
+        f2 x0, x1, y0, y1, z0, z1;   // per axis the (near, far) plane pairs of both children
+        int2 ch;
+        if constexpr (SRC == SRC_LDS && SCAN == SCAN_BVHQ) {
+          // node = the node's LDS address (the refs were relocated as the
+          // blob was copied): the axes one add each, the child refs at + 72
+          const LdsF2 lx = (LdsF2)(uintptr_t)(nof + offx), ly = (LdsF2)(uintptr_t)(nof + offy),
+                      lz = (LdsF2)(uintptr_t)(nof + offz);
+          x0 = lx[0], x1 = lx[1], y0 = ly[0], y1 = ly[1], z0 = lz[0], z1 = lz[1];
+          const long long c2 = *(LdsI64)(uintptr_t)(nof + 72);
+          ch = make_int2(static_cast<int>(c2), static_cast<int>(c2 >> 32));
+        } else {
+          const char* nb = reinterpret_cast<const char*>(nodes) + nof;
+          const f2* ax = reinterpret_cast<const f2*>(nb + offx);
+          const f2* ay = reinterpret_cast<const f2*>(nb + offy);
+          const f2* az = reinterpret_cast<const f2*>(nb + offz);
+          x0 = ax[0], x1 = ax[1], y0 = ay[0], y1 = ay[1], z0 = az[0], z1 = az[1];
+          ch = *reinterpret_cast<const int2*>(nb + 72);
+        }
         asm volatile("" : "+v"(r_xy), "+v"(r_z), "+v"(nf_x), "+v"(nf_y), "+v"(nf_z));
-        const f2 tnx = fma2(ax[0], bc_lo(r_xy), bc_lo(nf_x)), tfx = fma2(ax[1], bc_lo(r_xy), bc_hi(nf_x));
-        const f2 tny = fma2(ay[0], bc_hi(r_xy), bc_lo(nf_y)), tfy = fma2(ay[1], bc_hi(r_xy), bc_hi(nf_y));
-        const f2 tnz = fma2(az[0], bc_lo(r_z), bc_lo(nf_z)), tfz = fma2(az[1], bc_lo(r_z), bc_hi(nf_z));
+        const f2 tnx = fma2(x0, bc_lo(r_xy), bc_lo(nf_x)), tfx = fma2(x1, bc_lo(r_xy), bc_hi(nf_x));
+        const f2 tny = fma2(y0, bc_hi(r_xy), bc_lo(nf_y)), tfy = fma2(y1, bc_hi(r_xy), bc_hi(nf_y));
+        const f2 tnz = fma2(z0, bc_lo(r_z), bc_lo(nf_z)), tfz = fma2(z1, bc_lo(r_z), bc_hi(nf_z));
         tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
         const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
         const float tf1 = fminf(fminf(tfx.y, tfy.y), tfz.y);
-        // max(tn, t-min) as a bare v_max_f32: fmaxf re-canonicalises t-min
-        // (defined outside the loop) on every step, and the compiler folds
-        // med3(tn, t-min, +inf) back into that fmaxf. t-min is a product
-        // (canonical), and a NaN tn gives t-min either way (conservative).
-        float ntn0, ntn1;
-        asm("v_max_f32 %0, %1, %2" : "=v"(ntn0) : "v"(tn0), "v"(tmin));
-        asm("v_max_f32 %0, %1, %2" : "=v"(ntn1) : "v"(tn1), "v"(tmin));
-        hit0 = ntn0 <= fminf(tf0, best_t);
-        hit1 = ntn1 <= fminf(tf1, best_t);
+        // "[tn, tf] meets (tmin, best_t]" as max(tn, tmin) <= min(tf, best_t),
+        // spelled tn <= min(tf, best_t) and tmin <= tf (tmin < best_t always):
+        // a compare instead of a max per child.  Each is "not greater", so a
+        // NaN bound passes (conservative).
+        // (min(tf, best_t) as a bare v_min_f32: fminf would re-canonicalise
+        // best_t every step; a NaN tf gives best_t, conservative)
+        float tb0, tb1;
+        asm("v_min_f32 %0, %1, %2" : "=v"(tb0) : "v"(tf0), "v"(best_t));
+        asm("v_min_f32 %0, %1, %2" : "=v"(tb1) : "v"(tf1), "v"(best_t));
+        hit0 = !(tn0 > tb0) & !(tmin > tf0);
+        hit1 = !(tn1 > tb1) & !(tmin > tf1);
         c0 = ch.x;
         c1 = ch.y;
       };
       // the big bodies' leaves first: every lane, so a wave-uniform loop (their
       // hits, e.g. the ground, then cull the tree)
-      for (int b = 0; b < a.n_big_leaves; ++b) leaf(a.big_pair0 + b * leaf_pairs(SCAN));
+      for (int b = 0; b < a.n_big_leaves; ++b) {
+        if constexpr (kLeafRec)
+          leaf(static_cast<int>(lds_addr(nodes)) + a.bvh_off_pairs + ((a.big_pair0 >> 1) + b) * kLeafRecBytes);
+        else
+          leaf(a.big_pair0 + b * leaf_pairs(SCAN));
+      }
       if constexpr (SCAN == SCAN_BVHWW) {
         // speculative while-while (Aila & Laine 2009): a node phase in which
         // a lane that already holds a leaf keeps descending until every lane
@@ -1232,11 +1318,16 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           }
         }
       } else {
-      int node = 0;
+      // the root: the 4-body tree's refs are LDS addresses (relocated as copied)
+      int node = SRC == SRC_LDS && SCAN == SCAN_BVHQ ? static_cast<int>(lds_addr(nodes)) : 0;
       // the stack top as a pointer into the [entry][lane] stack: one add per
       // push / pop instead of index arithmetic
       StackT* const stk0 = s_stack + threadIdx.x;
       StackT* top = stk0;
+      // a row of the stack in bytes, held in a register the compiler cannot
+      // rematerialise (a literal would be moved into a VGPR on every push)
+      int row_b = 256 * static_cast<int>(sizeof(StackT));
+      asm volatile("" : "+v"(row_b));
       bool go = true;
       while (go) {
         if constexpr (STATS) {
@@ -1265,10 +1356,13 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         const bool sw = tn1 < tn0;
         int nxt = (i0 && (!i1 || !sw)) ? c0 : c1;
         *top = static_cast<StackT>(sw ? c0 : c1);
-        top += (i0 && i1) ? 256 : 0;
-        if (!(i0 || i1)) {   // pop, or (empty stack) leave with a harmless read of entry 0
-          go = top != stk0;
-          top -= go ? 256 : 0;
+        top = reinterpret_cast<StackT*>(reinterpret_cast<char*>(top) + ((i0 && i1) ? row_b : 0));
+        if (!(i0 || i1)) {
+          // pop, unconditionally: with an empty stack the top moves one row
+          // below the first entry, into the blob's last bytes (a harmless
+          // read), and the lane leaves -- one add and one compare, no select
+          top -= 256;
+          go = top >= stk0;
           nxt = *top;
         }
         node = nxt;
