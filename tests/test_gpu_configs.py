@@ -10,7 +10,9 @@ fp64 reference-semantics pin of the benchmark workload.
      r = 1 glass body bit-exact against the fp32 mirror at full spp;
   C3 3840x2160, 1000 spp, row tiles over 8 GPUs + host gather: rt_render's
      8-way fan-out (RT_FLAG_SHARDS_ON_DEVICE0 puts the 8 shards on this box's
-     one GPU) bit-identical to the 1-shard frame;
+     one GPU) bit-identical to the 1-shard frame, and two whole rows and two
+     64-pixel strips of the gathered frame (four shards) bit-exact against the
+     fp32 mirror at full spp;
   C4 7680x4320, 2000 spp, depth 64, 1000 bodies: the whole frame's
      properties, a row band re-rendered alone equal to the frame's rows, and
      eight 64-pixel strips bit-exact against the mirror at full spp; and C4's own
@@ -144,6 +146,16 @@ def test_c3_eight_shard_fan_out(gpu_lib):
     assert np.array_equal(one, eight)
     assert st1["samples"] == st8["samples"] == w * h * spp and st1["segments"] == st8["segments"]
     _props(one, st1, "c2")   # C3 renders C2's scene, camera and depth
+    # the gathered frame directly against the fp32 mirror at its full 1000
+    # spp: two whole rows from different shards (8-row tiles: rows 626 and
+    # 1507 are tiles 78 and 188, shards 6 and 4) -- the r = 1 glass body's
+    # centre row and the near field -- and 64-pixel strips of shards 0 and 7
+    bad = []
+    for r, c0, c1 in ((626, 0, w), (1507, 0, w), (3, 1900, 1964), (2159, 3776, 3840)):
+        ref, _, _ = _oracle(oracle.MODE_MIRROR32, sc, cam, w, h, spp, 50, rows=(r, r + 1), cols=(c0, c1))
+        if not np.array_equal(eight[r, c0:c1], ref[0, c0:c1]):
+            bad.append((r, c0))
+    assert not bad, bad
 
 
 def test_c4_full_frame(gpu_lib):
