@@ -2899,7 +2899,9 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
     vsel = (lds_of(ds.tree[1], 1) > kLds5 && ds.tree[2].n_nodes <= 256 &&
             lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
   if ((vsel == 18 || vsel == 19) && ds.tree[2].n_nodes > 256) vsel -= 2;   // u8 stack: 256 nodes at most
-  if ((vsel == 16 || vsel == 17) && ds.tree[1].n_nodes * 80 > 65535) vsel = 12;   // u16 stack of byte offsets
+  // u16 stack of node LDS addresses: the kernel's static LDS (< 4 KB; 8 KB
+  // allowed for) plus the node region must stay below 64 KB
+  if ((vsel == 16 || vsel == 17) && ds.tree[1].n_nodes * 80 + 8192 > 65535) vsel = 12;
   // the sorted kernels: the 4-body tree's byte-offset refs in a u16 stack
   // inside a wave's exchange slots, the blob beside the exchange buffer
   if ((vsel == 20 || vsel == 21) &&
