@@ -3106,7 +3106,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     if (rc != RT_OK) return rc;
   }
 #endif
+#ifdef RTCLJ_DIAG
+  // (diagnostic: RTCLJ_LDS_PAD bytes of dynamic LDS added to the launch, to
+  // measure the kernel at fewer workgroups per CU)
+  const size_t lds = launch_lds(*ds, vsel) + static_cast<size_t>(env_int("RTCLJ_LDS_PAD", 0, 0));
+#else
   const size_t lds = launch_lds(*ds, vsel);
+#endif
   if (lds > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   // the stream's entry: adaptive schedule and split partial sums
