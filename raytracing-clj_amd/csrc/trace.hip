@@ -308,11 +308,16 @@ __device__ __forceinline__ KArgsP kargs_opaque() {
 // ------------------------------------------------------------- kernel ----
 enum { SRC_LDS = 1, SRC_SCALAR = 2 };
 enum { SCAN_SIMPLE = 0, SCAN_GROUP4 = 1, SCAN_PK4 = 2, SCAN_BVH = 3, SCAN_BVHWW = 4, SCAN_BVHQ = 5, SCAN_BVHO = 6,
-       SCAN_BVHS = 7 /* sorted_kernel: 4-body leaves, 8 x 16 tiles, 512 threads */ };
+       SCAN_BVHS = 7 /* sorted_kernel: 4-body leaves, 8 x 16 tiles, 512 threads */,
+       SCAN_BVHQ7 = 8 /* BVHQ in a compact LDS image: seven workgroups per CU (variant 22) */ };
 // the traversal variants (BVHQ: ordered traversal of the 4-body-leaf tree)
-constexpr bool is_bvh_scan(int scan) { return scan >= SCAN_BVH && scan <= SCAN_BVHO; }
+constexpr bool is_bvh_scan(int scan) { return (scan >= SCAN_BVH && scan <= SCAN_BVHO) || scan == SCAN_BVHQ7; }
+// the 4-body-leaf ordered traversals: BVHQ, and BVHQ7 = the same walk with
+// a compact LDS image (u8 stack of node indices, u32 pixel sums, an 8-byte
+// pixel table): 23.0 KB for C1, seven workgroups per CU
+constexpr bool is_q(int scan) { return scan == SCAN_BVHQ || scan == SCAN_BVHQ7; }
 // body pairs per leaf of the tree a traversal variant walks
-constexpr int leaf_pairs(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_BVHQ ? 2 : 1; }
+constexpr int leaf_pairs(int scan) { return scan == SCAN_BVHO ? 4 : is_q(scan) ? 2 : 1; }
 
 // two bodies side by side for packed fp32 math (v_pk_*_f32: one IEEE op per half)
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -353,7 +358,9 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_
 // CU).  Without the bound the unit loop's longer-lived uniform values
 // (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
 // waves; with it, a few of them spill to scratch outside the hot loop.
-constexpr int min_waves(int scan, bool stats) { return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHO ? 5 : 1; }
+constexpr int min_waves(int scan, bool stats) {
+  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 5 : 1;
+}
 
 template <int SRC, int SCAN, bool STATS = false>
 __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(const KArgs a) {
@@ -391,7 +398,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
 #endif
   constexpr int TH = tile_rows(SCAN);   // tile rows
   constexpr int NPX = kTile * TH;       // pool pixels
-  __shared__ unsigned long long s_acc[NPX * 3];
+  // the pool's pixel sums: u32 in the compact variant (the host runs it only
+  // when a sample's colour is <= 1 per channel and spp <= 255: a sum stays
+  // below 255 * 2^24 < 2^32), u64 otherwise
+  using AccT = std::conditional_t<SCAN == SCAN_BVHQ7, unsigned, unsigned long long>;
+  __shared__ AccT s_acc[NPX * 3];
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
   uint64_t st_trav = 0, st_trav_lanes = 0;   // BVH: wave-level traversal iterations, lanes in them
   uint64_t st_leafw = 0, st_consw = 0;        // BVH: wave-level leaf passes, exact-test passes
@@ -470,7 +481,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   }
   // the scene image (a thief only once it has samples to run)
   if constexpr (SRC == SRC_LDS) {
-    if constexpr (SCAN == SCAN_BVHQ) {
+    if constexpr (is_q(SCAN)) {
       // the 4-body tree's inner-child refs (node byte offsets in the blob)
       // become LDS addresses as they are copied: a node step then reads its
       // child refs at ref + 72 and its planes at ref + the ray's plane
@@ -490,8 +501,10 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         if (i < nodes_f4) {
           if (i % 5 == 4) {
             const int r0 = __float_as_int(v.z), r1 = __float_as_int(v.w);
-            v.z = __int_as_float(r0 >= 0 ? r0 + nb0 : ~(rec0 + (~r0 >> 1) * kLeafRecBytes));
-            v.w = __int_as_float(r1 >= 0 ? r1 + nb0 : ~(rec0 + (~r1 >> 1) * kLeafRecBytes));
+            // (the compact variant's inner refs: node indices, for its u8 stack)
+            const int in0 = SCAN == SCAN_BVHQ7 ? r0 / 80 : r0 + nb0, in1 = SCAN == SCAN_BVHQ7 ? r1 / 80 : r1 + nb0;
+            v.z = __int_as_float(r0 >= 0 ? in0 : ~(rec0 + (~r0 >> 1) * kLeafRecBytes));
+            v.w = __int_as_float(r1 >= 0 ? in1 : ~(rec0 + (~r1 >> 1) * kLeafRecBytes));
           }
         } else if (i < nodes_f4 + pairs_f4) {   // pair k / 2, half k % 2
           const int k = i - nodes_f4, pr = k >> 1;
@@ -514,7 +527,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // (u8 entries for the 8-body-leaf traversal, whose trees the host caps at
   // 256 nodes: with its u16 body indices this keeps a 1000-body scene's
   // image under the 32 KB that 5 workgroups per CU allow)
-  using StackT = std::conditional_t<SCAN == SCAN_BVHO, unsigned char, unsigned short>;
+  using StackT = std::conditional_t<SCAN == SCAN_BVHO || SCAN == SCAN_BVHQ7, unsigned char, unsigned short>;
   StackT* s_stack = reinterpret_cast<StackT*>(
       reinterpret_cast<char*>(s_geo) + (SRC == SRC_LDS ? ka->bvh_blob_f4 * 16 : 0));
 
@@ -608,20 +621,25 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     s_mb_take[threadIdx.x] = 0;
     s_mb_lim[threadIdx.x] = ka->compact > 0 ? ka->compact : -1;
   }
-  if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0ull;
+  if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0;
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
   // image has no room for it: C4 keeps 5 workgroups per CU)
-  constexpr bool kPixelTable = SCAN == SCAN_BVHQ && !kRing;
-  __shared__ float4 s_px[kPixelTable ? NPX : 1];
+  constexpr bool kPixelTable = is_q(SCAN) && !kRing;
+  // (the compact variant: key and (x | y << 16) in 8 bytes)
+  using PxT = std::conditional_t<SCAN == SCAN_BVHQ7, uint2, float4>;
+  __shared__ PxT s_px[kPixelTable ? NPX : 1];
   if constexpr (kPixelTable) {
     const int t = static_cast<int>(threadIdx.x);
     if (t < npx) {
       const int qy = vw == 1 ? t : static_cast<int>(__umulhi(static_cast<uint32_t>(t), mag_vw));
       const int px = qx0 + (t - qy * vw);
       const int gy = image_row(qy0 + qy);
-      s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
+      if constexpr (SCAN == SCAN_BVHQ7)
+        s_px[t] = make_uint2(pixel_key(px, gy), static_cast<unsigned>(px) | (static_cast<unsigned>(gy) << 16));
+      else
+        s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
     }
   }
   __syncthreads();
@@ -919,7 +937,12 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       q = j - k * npx;
       uint32_t pk;
       float fpx, fgy;
-      if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
+      if constexpr (kPixelTable && SCAN == SCAN_BVHQ7) {
+        const uint2 pt = s_px[q];
+        pk = pt.x;
+        fpx = static_cast<float>(pt.y & 0xffffu);
+        fgy = static_cast<float>(pt.y >> 16);
+      } else if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
         const float4 pt = s_px[q];
         pk = __float_as_uint(pt.x);
         fpx = pt.y;
@@ -1096,7 +1119,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // a leaf: one pair (leaf size 2) or two consecutive pairs (BVHQ, leaf
       // size 4), tested packed; the acceptance is order-independent
       // (the 4-body tree in LDS: p is a leaf record's LDS address, see the copy)
-      constexpr bool kLeafRec = SRC == SRC_LDS && SCAN == SCAN_BVHQ;
+      constexpr bool kLeafRec = SRC == SRC_LDS && is_q(SCAN);
       auto leaf = [&](int p) {
         if constexpr (STATS) {
           ++st_blk;
@@ -1204,10 +1227,14 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
         // the 4-body tree's inner-child refs are byte offsets (node * 80,
         // written by rt_scene_upload): no multiply per step
-        const unsigned nof = SCAN == SCAN_BVHQ ? static_cast<unsigned>(node) : __umul24(static_cast<unsigned>(node), 80u);
+        // (BVHQ: node is the node's LDS address; BVHQ7: its index, the
+        // address one multiply-add away; others: an index into nodes)
+        const unsigned nof = SCAN == SCAN_BVHQ    ? static_cast<unsigned>(node)
+                             : SCAN == SCAN_BVHQ7 ? __umul24(static_cast<unsigned>(node), 80u) + lds_addr(nodes)
+                                                  : __umul24(static_cast<unsigned>(node), 80u);
         f2 x0, x1, y0, y1, z0, z1;   // per axis the (near, far) plane pairs of both children
         int2 ch;
-        if constexpr (SRC == SRC_LDS && SCAN == SCAN_BVHQ) {
+        if constexpr (SRC == SRC_LDS && is_q(SCAN)) {
           // node = the node's LDS address (the refs were relocated as the
           // blob was copied): the axes one add each, the child refs at + 72
           const LdsF2 lx = (LdsF2)(uintptr_t)(nof + offx), ly = (LdsF2)(uintptr_t)(nof + offy),
@@ -1319,7 +1346,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         }
       } else {
       // the root: the 4-body tree's refs are LDS addresses (relocated as copied)
-      int node = SRC == SRC_LDS && SCAN == SCAN_BVHQ ? static_cast<int>(lds_addr(nodes)) : 0;
+      int node = SRC == SRC_LDS && SCAN == SCAN_BVHQ ? static_cast<int>(lds_addr(nodes)) : 0;   // (BVHQ7: index 0)
       // the stack top as a pointer into the [entry][lane] stack: one add per
       // push / pop instead of index arithmetic
       StackT* const stk0 = s_stack + threadIdx.x;
@@ -1580,13 +1607,10 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     }
     if (done) {   // the sample's colour into its pixel's fixed-point sum (order-free)
       if constexpr (STATS) st_fl += 3;
-      unsigned long long* acc = &s_acc[q * 3];
-      __hip_atomic_fetch_add(acc + 0, static_cast<unsigned long long>(fix24(cr)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(acc + 1, static_cast<unsigned long long>(fix24(cg)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(acc + 2, static_cast<unsigned long long>(fix24(cb)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      AccT* acc = &s_acc[q * 3];
+      __hip_atomic_fetch_add(acc + 0, static_cast<AccT>(fix24(cr)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(acc + 1, static_cast<AccT>(fix24(cg)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(acc + 2, static_cast<AccT>(fix24(cb)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     // refill: the lanes whose paths ended take their next indices
     const uint64_t m = __ballot(done);
@@ -1699,16 +1723,17 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   };
   if (split) {   // one split's integer sums, added to the tile's (order-free); finalize_kernel converts them
     if (t < npx * 3 && s_acc[t])
-      __hip_atomic_fetch_add(&ke->part[out_index(t)], s_acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&ke->part[out_index(t)], static_cast<unsigned long long>(s_acc[t]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   } else if (alone) {   // every sample of the tile was this workgroup's
-    if (t < npx * 3) write_mean(out_index(t), s_acc[t]);
+    if (t < npx * 3) write_mean(out_index(t), static_cast<unsigned long long>(s_acc[t]));
   } else {
     // a shared tile (owner or helper): the integer sums
     // meet in sum[tile] (atomics: any order, the same total); the workgroup
     // whose samples complete the pool converts them and re-zeroes the slots
     unsigned long long* gs = ke->sum + static_cast<size_t>(tile) * (NPX * 3);
     if (t < npx * 3 && s_acc[t])
-      __hip_atomic_fetch_add(&gs[t], s_acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&gs[t], static_cast<unsigned long long>(s_acc[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -2497,7 +2522,7 @@ struct Variant {
   int scan;   // SCAN_* (the tile shape: tile_rows)
   int threads = 256;   // workgroup size
 };
-constexpr int kVariants = 22;
+constexpr int kVariants = 23;
 // the tree a traversal variant walks: 0 = 2-body leaves, 1 = 4, 2 = 8
 static int variant_tree(int v) { return v >= 20 ? 1 : v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 #define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
@@ -2552,6 +2577,9 @@ static const Variant& variant_table(int v) {
 #else
       none, none,
 #endif
+      // 16's walk in a compact LDS image, seven workgroups per CU (explicit
+      // selection; rt_launch falls back to 16 unless compact_ok holds)
+      {RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7},        // 22
   };
   return (v >= 0 && v < kVariants) ? t[v] : none;
 }
@@ -2675,6 +2703,7 @@ struct rt_dscene {
   float4* sph;
   float4* mat;
   int* kind;
+  bool unit_albedo;            // every lambertian/metal albedo channel within [-1, 1] (compact_ok)
   mutable ScheduleSet sched;   // rt_launch's adaptive tile order
 };
 
@@ -2793,6 +2822,11 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
   d->device = device;
   d->n = n;
   d->n_pad = n_pad;
+  d->unit_albedo = true;
+  for (int i = 0; i < n; ++i)
+    if (s->mat_kind[i] == RT_LAMBERTIAN || s->mat_kind[i] == RT_METAL)
+      for (int c = 0; c < 3; ++c)
+        if (!(std::fabs(s->mat[4 * i + c]) <= 1.0f)) d->unit_albedo = false;
   // BVHs over the bodies (the traversal variants), the three trees built
   // concurrently on host threads (C1: 2.4 -> ~1 ms of a first rt_render)
   BvhHost bvhs[3];
@@ -2884,6 +2918,12 @@ static size_t stack_of(const DTree& t, int tree) {
   return static_cast<size_t>(stack_entries(t, tree)) * 256 * (tree == 2 ? 1 : 2);
 }
 static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
+// variant 22 (the compact image): u8 node indices, depth rows (the dead
+// far-child write goes one above the top, as in 16)
+static int stack_entries_compact(const DTree& t) { return std::max(t.depth, 1); }
+static size_t lds_of_compact(const DTree& t) {
+  return static_cast<size_t>(t.blob_f4) * 16 + static_cast<size_t>(stack_entries_compact(t)) * 256;
+}
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
 // kernel's static LDS (pool counter, the 64 pixels' colour sums and pixel
 // table).  (Its registers allow 6; C1's 24.0 KB image fits 6 as well.)
@@ -2914,6 +2954,26 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
     if (vsel != 12 && lds_of(t, variant_tree(vsel)) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
     if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
   }
+  if (vsel == 22 && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
+  return vsel;
+}
+
+// The compact variant (22) for a launch: the 4-body tree's node indices fit
+// a byte, and a pixel's u32 sum cannot overflow -- every sample's colour is
+// at most 1 per channel (albedos within [-1, 1]: the sky and the dielectric
+// give at most 1) and a pixel gets at most spp <= 255 samples, 255 * 2^24 <
+// 2^32.  Selected explicitly (rt_set_variant(22)); where it does not apply
+// the launch runs 16.  Seven workgroups per CU instead of six, but C1 gains
+// only 0.3 % (5.888 vs 5.907 ms) and its first frame loses 0.5 %: the
+// 7th wave's latency hiding is spent on 14 spilled VGPRs and a multiply-add
+// per node step (profiles/r04/w7/), so 16 stays the default.
+static bool compact_ok(const rt_dscene& ds, const rt_params& p) {
+  return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp <= 255 && ds.tree[1].depth + 2 <= kBvhStack;
+}
+static int launch_variant(const rt_dscene& ds, const rt_params& p) {
+  const int sel = g_variant.load();
+  int vsel = resolve_variant(ds, sel);
+  if (vsel == 22) vsel = compact_ok(ds, p) ? 22 : 16;
   return vsel;
 }
 
@@ -2923,6 +2983,7 @@ extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_var
 static size_t launch_lds(const rt_dscene& ds, int vsel) {
   const Variant& v = variant_table(vsel);
   if (v.scan == SCAN_BVHS) return static_cast<size_t>(ds.tree[1].blob_f4) * 16 + kXBytes;   // blob | exchange
+  if (vsel == 22) return lds_of_compact(ds.tree[1]);
   if (vsel >= 11) {
     const DTree& tr = ds.tree[variant_tree(vsel)];
     return v.lds ? lds_of(tr, variant_tree(vsel)) : stack_of(tr, variant_tree(vsel));
@@ -2938,7 +2999,7 @@ extern "C" int rt_launch_occupancy(const rt_dscene* ds, const rt_params* p, int*
   const int rows = rows_out(*p);
   if (rows <= 0 || p->width <= 0) return set_error(RT_E_ARG, "rt_launch_occupancy: empty frame");
   HIP_TRY(hipSetDevice(ds->device));
-  const int vsel = resolve_variant(*ds, g_variant.load());
+  const int vsel = launch_variant(*ds, *p);
   const void* fn = variant_table(vsel).fn;
   if (!fn) return set_error(RT_E_ARG, "rt_launch_occupancy: no kernel for variant " + std::to_string(vsel));
   const size_t lds = launch_lds(*ds, vsel);
@@ -3065,7 +3126,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
-  int vsel = resolve_variant(*ds, g_variant.load());
+  int vsel = launch_variant(*ds, *p);
   if (variant_table(vsel).scan == SCAN_BVHS && p->max_depth > 1023) vsel = 16;   // (a path's depth left: 10 bits in the exchange)
   const Variant& v = variant_table(vsel);
   if (!v.fn) return set_error(RT_E_ARG, "rt_launch: no kernel for variant " + std::to_string(vsel));
@@ -3079,13 +3140,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // entries per lane: the ordered traversal (trees 1, 2) holds at most depth
   // (a node on level L has L - 1 ancestors; the dead far-child write goes one
   // above them); tree 0 also serves the while-while variants (depth + 2)
-  a.bvh_stack = stack_entries(tr, variant_tree(vsel));
+  a.bvh_stack = vsel == 22 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   // drain compaction: a post holds as many paths as a wave's stack slice has
   // room for (RTCLJ_COMPACT: post at or below that many paths; 0 off)
   {
-    const int words = a.bvh_stack * 16 * (v.scan == SCAN_BVHO ? 1 : 2);   // a wave's stack slice
+    const int words = a.bvh_stack * 16 * (v.scan == SCAN_BVHO || v.scan == SCAN_BVHQ7 ? 1 : 2);   // a wave's stack slice
     a.mb_paths = std::min(32, words / kMbFields);
     a.compact = is_bvh_scan(v.scan) ? std::min(a.mb_paths, env_int("RTCLJ_COMPACT", a.mb_paths, 0)) : 0;
   }

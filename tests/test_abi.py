@@ -144,7 +144,7 @@ def test_version_and_variant():
     from rtclj._lib import diag_lib
     assert b"gfx950" in rtclj.lib.rt_version()
     # the product build holds the default traversal and its fallbacks only
-    for v in (5, 12, 16, 18):
+    for v in (5, 12, 16, 18, 22):
         old = rtclj.lib.rt_set_variant(v)
         assert rtclj.lib.rt_set_variant(old) == v
     for v in (2, 3, 11, 17, 99, -1):
@@ -152,9 +152,9 @@ def test_version_and_variant():
     assert rtclj.lib.rt_set_variant(0) == 0
     # the diagnostic build holds every variant
     d = diag_lib()
-    for v in range(1, 20):
+    for v in list(range(1, 20)) + [22]:
         assert d.rt_set_variant(v) >= 0
-    assert d.rt_set_variant(0) == 19
+    assert d.rt_set_variant(0) == 22
     assert rtclj.lib.rt_resolve_variant(None) == -1
     out4 = (C.c_int * 4)()
     assert rtclj.lib.rt_launch_occupancy(None, None, out4) < 0   # NULL scene: error, no device call

@@ -18,7 +18,7 @@ TOL_ABS = 1e-4
 TOL_FRAC = 0.995
 
 
-PRODUCT_VARIANTS = (0, 5, 12, 16, 18)
+PRODUCT_VARIANTS = (0, 5, 12, 16, 18, 22)
 
 
 class variant:
@@ -297,7 +297,7 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("v", [11, 12, 14, 16, 18])
+@pytest.mark.parametrize("v", [11, 12, 14, 16, 18, 22])
 def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, v):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
@@ -352,7 +352,7 @@ def test_bvh_small_scenes(gpu_lib, n):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
     out = {}
-    for v in (5, 11, 16, 18):
+    for v in (5, 11, 16, 18, 22):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5, library=dll)
     assert np.array_equal(out[5], out[11])
@@ -385,10 +385,10 @@ def test_bvh_big_bodies(gpu_lib, n_big):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(64, 36, **R.REFERENCE_CAMERA)
     out = {}
-    for v in (5, 11, 16, 18):
+    for v in (5, 11, 16, 18, 22):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 64, 36, spp=8, max_depth=20, seed=9, library=dll)
-    for v in (11, 16, 18):
+    for v in (11, 16, 18, 22):
         assert np.array_equal(out[5], out[v]), v
     ref, _, _ = _mirror(sc, cam, 64, 36, 8, 20, seed=9)
     assert np.array_equal(out[5], ref)
@@ -411,7 +411,7 @@ def test_bvh_cover16_u8_stack_and_u16_indices(gpu_lib):
     finally:
         lib.rt_scene_free(ds)
     out = {}
-    for v in (5, 16, 18):
+    for v in (5, 16, 18, 22):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 96, 54, spp=6, max_depth=64, seed=4, library=dll)
     assert np.array_equal(out[5], out[16])
@@ -453,7 +453,7 @@ def test_bvh_8body_tree_over_256_nodes_uses_4body(gpu_lib):
     assert np.array_equal(out[5], out[18])
 
 
-@pytest.mark.parametrize("vsel", [0, 11, 16, 18])
+@pytest.mark.parametrize("vsel", [0, 11, 16, 18, 22])
 def test_bvh_large_scene_falls_back(gpu_lib, vsel):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
     the global-memory traversal of the 2-body tree: same bits as the scan."""
@@ -484,7 +484,7 @@ def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
     return out, segs, smp
 
 
-@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18])
+@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18, 22])
 def test_realm_flag_matches_mirror(gpu_lib, vsel):
     """RT_FLAG_REALM (realm.raytracing semantics) through the kernel == the
     oracle's MODE_REALM32, bit for bit: the realm scene and the cover scene."""
@@ -529,3 +529,43 @@ def test_realm_shards_and_fixture(gpu_lib):
     d = np.abs(blocks - np.array(st["blocks"]))
     assert d.mean() <= 0.25 and d.max() <= 2.5, (d.mean(), d.max())
     assert np.abs(rgb - pix).mean() <= 3.5
+
+
+def test_compact_variant_limits(gpu_lib):
+    """Variant 22 (the 4-body walk in a compact LDS image: u8 node-index
+    stack, u32 pixel sums, seven workgroups per CU), when selected, runs only
+    where a u32 sum cannot overflow: spp <= 255 and every albedo within
+    [-1, 1]. At spp 255 -- the largest sums -- it equals the mirror bit for
+    bit; at 256, or with an albedo above 1, the launch runs 16 (u64 sums).
+    The default selector keeps 16."""
+    import ctypes as C
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import check, lib, rt_params
+
+    def launch_variant(sc, w, h, spp):
+        ds = C.c_void_p()
+        check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+        try:
+            p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=50, seed=1)
+            o = (C.c_int * 4)()
+            check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+            return o[3], o[0]
+        finally:
+            lib.rt_scene_free(ds)
+
+    sc = scenes.cover(11)
+    assert launch_variant(sc, 1200, 675, 100) == (16, 6)   # the default
+    with variant(22):
+        assert launch_variant(sc, 1200, 675, 100) == (22, 7)
+        assert launch_variant(sc, 1200, 675, 255)[0] == 22
+        assert launch_variant(sc, 1200, 675, 256)[0] == 16
+        hot = R.Scene(sc.sphere.copy(), sc.kind.copy(), sc.mat.copy())
+        lam = np.nonzero(hot.kind == 0)[0]   # (RT_LAMBERTIAN)
+        hot.mat[lam[0], 0] = 1.5                      # one albedo channel above 1
+        assert launch_variant(hot, 1200, 675, 100)[0] == 16
+        # spp 255 on a small cover frame: the u32 sums at their largest
+        cam = scenes.cover_camera(160, 90)
+        g = R.render(sc, cam, 160, 90, spp=255, seed=3)
+    ref, _, _ = _mirror(sc, cam, 160, 90, 255, 50, seed=3)
+    assert np.array_equal(g, ref)
