@@ -2514,6 +2514,9 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //   11 BVH in LDS, 2-body leaves     13 = 11 + stats
 //   14 11 with a speculative while-while traversal           15 = 14 + stats
 //   17 = 16 + stats                  19 = 18 + stats
+//   20 / 21 direction-coherent waves (sorted_kernel)
+// Both builds: 22 = 16 in a compact LDS image, seven workgroups per CU
+// (explicit selection; spp <= 255, albedos in [-1, 1], <= 256 tree nodes).
 // Every variant renders the same bits.
 struct Variant {
   const void* fn;
