@@ -267,13 +267,14 @@ int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_params* p,
 int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_stream);
 
 /* Kernel variant selector (all variants give identical bits).  The product
- * library holds: 0 = default (16, or 18 when the 4-body tree's LDS image
- * would cap a CU below 5 workgroups and the 8-body tree's is smaller);
+ * library holds: 0 = default (22 where it applies, else 16; 18 when the
+ * 4-body tree's LDS image would cap a CU below 5 workgroups and the 8-body
+ * tree's is smaller);
  * 16 = BVH traversal, 4 bodies per leaf, nodes and leaf bodies in LDS;
  * 18 = the same with 8 bodies per leaf; 22 = 16 in a compact LDS image (u8
- * node-index stack, u32 pixel sums: seven workgroups per CU; used only where
- * spp <= 255, every albedo lies in [-1, 1] and the tree has <= 256 nodes,
- * else the launch runs 16); 12 = BVH with 2 bodies per leaf read
+ * node-index stack, u32 pixel sums: seven workgroups per CU; 0 selects it
+ * wherever spp <= 255, every albedo lies in [-1, 1] and the tree has <= 256
+ * nodes, else 16); 12 = BVH with 2 bodies per leaf read
  * from global memory (the fallback for a tree too big for LDS); 5 = linear
  * scan, bodies in groups of 4 through the scalar cache (the fallback for a
  * tree too deep for the stack).  The diagnostic build lib/librtclj_diag.so

@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     ++segs;
     const float len = sqrt_rn(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
     const float il = 1.0f / len;                              // vec3a/unit as d * (1/|d|)
-    const float ux = dx * il, uy = dy * il, uz = dz * il;
+    float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
     if constexpr (STATS) st_fl += 11;                         // |d|, 1/|d|, u, t-min
     float best_t = INFINITY;
@@ -1395,6 +1395,15 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         node = nxt;
       }
       }
+      // the ray's origin and unit direction again from the packed copies the
+      // walk used (the same values): the scalar ones are dead through it,
+      // six VGPRs fewer at its peak
+      ox = o_xy.x;
+      oy = o_xy.y;
+      oz = o_zux.x;
+      ux = o_zux.y;
+      uy = u_yz.x;
+      uz = u_yz.y;
     } else if constexpr (SCAN == SCAN_PK4) {
       // As SCAN_GROUP4, but the arithmetic of two bodies runs in one packed
       // instruction (v_pk_add/mul/fma_f32: each half is the same IEEE-rounded
@@ -2504,7 +2513,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //   16 BVH in LDS, 4-body leaves (two pairs)      18 BVH in LDS, 8-body leaves
 //   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
 //    5 linear scan, grouped, table through the scalar cache: a tree too deep
-//    0 = default (16, or 18 when the 4-body tree's LDS image is large)
+//    0 = default (22 where it applies, else 16; 18 when the 4-body tree's LDS image is large)
 // The diagnostic build (-DRTCLJ_DIAG, lib/librtclj_diag.so) adds the A/B and
 // statistics variants:
 //    1 LDS table, simple scan         2 scalar-cache table, simple scan
@@ -2516,7 +2525,8 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //   17 = 16 + stats                  19 = 18 + stats
 //   20 / 21 direction-coherent waves (sorted_kernel)
 // Both builds: 22 = 16 in a compact LDS image, seven workgroups per CU
-// (explicit selection; spp <= 255, albedos in [-1, 1], <= 256 tree nodes).
+// (the default where spp <= 255, albedos lie in [-1, 1] and the tree has
+// <= 256 nodes; 16 elsewhere).
 // Every variant renders the same bits.
 struct Variant {
   const void* fn;
@@ -2580,8 +2590,8 @@ static const Variant& variant_table(int v) {
 #else
       none, none,
 #endif
-      // 16's walk in a compact LDS image, seven workgroups per CU (explicit
-      // selection; rt_launch falls back to 16 unless compact_ok holds)
+      // 16's walk in a compact LDS image, seven workgroups per CU (the
+      // default where compact_ok holds; rt_launch falls back to 16 elsewhere)
       {RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7},        // 22
   };
   return (v >= 0 && v < kVariants) ? t[v] : none;
@@ -2965,18 +2975,17 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
 // a byte, and a pixel's u32 sum cannot overflow -- every sample's colour is
 // at most 1 per channel (albedos within [-1, 1]: the sky and the dielectric
 // give at most 1) and a pixel gets at most spp <= 255 samples, 255 * 2^24 <
-// 2^32.  Selected explicitly (rt_set_variant(22)); where it does not apply
-// the launch runs 16.  Seven workgroups per CU instead of six, but C1 gains
-// only 0.3 % (5.888 vs 5.907 ms) and its first frame loses 0.5 %: the
-// 7th wave's latency hiding is spent on 14 spilled VGPRs and a multiply-add
-// per node step (profiles/r04/w7/), so 16 stays the default.
+// 2^32.  The default selector runs it wherever it applies (and an explicit
+// 22 too); elsewhere the launch runs 16.  Seven workgroups per CU instead of
+// six, in 72 VGPRs without a spill: C1 5.90 -> 5.83 ms (profiles/r04/w7/,
+// DESIGN.md §8.1).
 static bool compact_ok(const rt_dscene& ds, const rt_params& p) {
   return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp <= 255 && ds.tree[1].depth + 2 <= kBvhStack;
 }
 static int launch_variant(const rt_dscene& ds, const rt_params& p) {
   const int sel = g_variant.load();
   int vsel = resolve_variant(ds, sel);
-  if (vsel == 22) vsel = compact_ok(ds, p) ? 22 : 16;
+  if ((sel == 0 && vsel == 16) || vsel == 22) vsel = compact_ok(ds, p) ? 22 : 16;
   return vsel;
 }
 

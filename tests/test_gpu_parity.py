@@ -555,7 +555,8 @@ def test_compact_variant_limits(gpu_lib):
             lib.rt_scene_free(ds)
 
     sc = scenes.cover(11)
-    assert launch_variant(sc, 1200, 675, 100) == (16, 6)   # the default
+    assert launch_variant(sc, 1200, 675, 100) == (22, 7)   # the default where it applies
+    assert launch_variant(sc, 1200, 675, 500)[0] == 16
     with variant(22):
         assert launch_variant(sc, 1200, 675, 100) == (22, 7)
         assert launch_variant(sc, 1200, 675, 255)[0] == 22
