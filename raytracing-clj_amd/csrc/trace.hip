@@ -279,7 +279,7 @@ constexpr int kShareBatch = 128;
 // word f * P + p (field f of path p, P paths per post) at entry row
 // (f * P + p) / W, word (f * P + p) % W of the wave's W = 16 x sizeof(entry)
 // words in that row.  P = as many as the slice holds, 13 fields each (C1's
-// depth-9 u16 stack: 22; at most 32).
+// depth-9 u16 stack: 22, its u8 one in variant 22: 11; at most 32).
 constexpr int kMbFields = 13;
 // stats builds / RTCLJ_TIMELINE: waves recorded per launch (dispatch slot order)
 constexpr int kDbgWaves = 1 << 17;
