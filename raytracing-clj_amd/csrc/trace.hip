@@ -1161,10 +1161,17 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
             id = li[hb + q];
           }
           asm volatile("" : "+v"(o_xy), "+v"(o_zux), "+v"(u_yz));
-          const f2 ocx = g.x - bc_lo(o_xy), ocy = g.y - bc_hi(o_xy), ocz = g.z - bc_lo(o_zux);
-          const f2 h = fma2(bc_hi(u_yz), ocz, fma2(bc_lo(u_yz), ocy, bc_hi(o_zux) * ocx));
-          const f2 c = fma2(ocx, ocx, fma2(ocz, ocz, fma2(ocy, ocy, g.w)));
-          const f2 disc = fma2(h, h, -c);
+          // (scalar fp32 per body, not v_pk_*: a packed op issues on one VALU
+          // port only, two v_fma_f32 dual-issue -- 5.84 -> 5.45 ms on C1
+          // with the node step's planes, profiles/r05/unpack/)
+          f2 h, c, disc;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float ocx = g.x[e] - o_xy.x, ocy = g.y[e] - o_xy.y, ocz = g.z[e] - o_zux.x;
+            h[e] = fmaf(u_yz.y, ocz, fmaf(u_yz.x, ocy, o_zux.y * ocx));
+            c[e] = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w[e])));
+            disc[e] = fmaf(h[e], h[e], -c[e]);
+          }
           hh[2 * q] = h.x;
           hh[2 * q + 1] = h.y;
           dd[2 * q] = disc.x;
@@ -1251,9 +1258,17 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           ch = *reinterpret_cast<const int2*>(nb + 72);
         }
         asm volatile("" : "+v"(r_xy), "+v"(r_z), "+v"(nf_x), "+v"(nf_y), "+v"(nf_z));
-        const f2 tnx = fma2(x0, bc_lo(r_xy), bc_lo(nf_x)), tfx = fma2(x1, bc_lo(r_xy), bc_hi(nf_x));
-        const f2 tny = fma2(y0, bc_hi(r_xy), bc_lo(nf_y)), tfy = fma2(y1, bc_hi(r_xy), bc_hi(nf_y));
-        const f2 tnz = fma2(z0, bc_lo(r_z), bc_lo(nf_z)), tfz = fma2(z1, bc_lo(r_z), bc_hi(nf_z));
+        // (per child scalar v_fma_f32: dual-issued, unlike v_pk_fma_f32)
+        f2 tnx, tfx, tny, tfy, tnz, tfz;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          tnx[e] = fmaf(x0[e], r_xy.x, nf_x.x);
+          tfx[e] = fmaf(x1[e], r_xy.x, nf_x.y);
+          tny[e] = fmaf(y0[e], r_xy.y, nf_y.x);
+          tfy[e] = fmaf(y1[e], r_xy.y, nf_y.y);
+          tnz[e] = fmaf(z0[e], r_z.x, nf_z.x);
+          tfz[e] = fmaf(z1[e], r_z.x, nf_z.y);
+        }
         tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
         const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
