@@ -288,9 +288,12 @@ int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_s
  * process (an atomic, read once per launch). */
 int rt_set_variant(int variant);
 
-/* The kernel variant rt_launch would run for ds under the current selector
- * (the default resolved for this scene, or a fallback when a tree does not
- * fit): for reading the matching statistics build.  -1 on a NULL scene. */
+/* The kernel variant the current selector resolves to for ds (the default
+ * resolved for this scene, or a fallback when a tree does not fit), before
+ * the per-launch choice between 16 and its compact image 22, which also
+ * depends on the launch (spp <= 255, frame size): rt_launch_occupancy's
+ * out4[3] reports the variant a given launch runs.  For reading the matching
+ * statistics build.  -1 on a NULL scene. */
 int rt_resolve_variant(const rt_dscene* ds);
 
 /* Occupancy of the launch rt_launch would make for (ds, p) under the current

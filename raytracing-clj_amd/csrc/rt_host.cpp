@@ -287,9 +287,10 @@ struct Ctx {
   size_t u8_cap = 0;
   uint64_t* d_cnt = nullptr;
   uint64_t* h_cnt = nullptr;  // pinned
-  std::vector<const void*> scenes;   // device scenes launched on (their per-stream schedule entries)
-  void launched(const void* ds) {
-    if (std::find(scenes.begin(), scenes.end(), ds) == scenes.end()) scenes.push_back(ds);
+  std::vector<uint64_t> scenes;   // upload ids of the device scenes launched on (their per-stream schedule entries)
+  void launched(const rt_dscene* ds) {
+    const uint64_t id = scene_uid(ds);
+    if (std::find(scenes.begin(), scenes.end(), id) == scenes.end()) scenes.push_back(id);
   }
   ~Ctx() {
     (void)hipSetDevice(device);

@@ -40,11 +40,15 @@ int rows_out(const rt_params& p);
 // them; those no longer live are skipped), so the scenes' per-stream slots do
 // not fill up with dead streams -- and a direct rt_launch user's entries on a
 // stream the context shared (the NULL stream) are left alone (trace.hip).
-void release_stream_schedules(void* stream, const void* const* scenes, int n);
+// Scenes are named by their upload id (scene_uid), never by address: a freed
+// scene's address can come back for a new one.
+void release_stream_schedules(void* stream, const uint64_t* scene_uids, int n);
 // A context that moves from the NULL stream to a stream of its own keeps its
 // adaptive tile orders: the entries of `from` in those scenes become `to`'s
 // (both streams idle; a scene that already has an entry for `to` keeps it).
-void rebind_stream_schedules(void* from, void* to, const void* const* scenes, int n);
+void rebind_stream_schedules(void* from, void* to, const uint64_t* scene_uids, int n);
+// A device scene's upload id: unique for the process's lifetime.
+uint64_t scene_uid(const rt_dscene* ds);
 
 // rt_quantize's byte of one channel as 255 thresholds: t[q] (q = 1..255) is
 // the smallest float whose byte is >= q (t[0] unused), so a channel's byte is

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <iterator>
 #include <string>
 #include <thread>
 #include <utility>
@@ -49,8 +50,20 @@ int main(int argc, char** argv) {
   int ndev = 0;
   double device_count_ms = 0.0, prep_ms[4] = {0, 0, 0, 0};
   int gpus_arg = 0;
-  for (int i = 1; i + 1 < argc; ++i)
+  // (a missing option value ends the process before the start-up thread
+  // exists: no exit while that thread may be inside the HIP runtime)
+  static const char* const kValued[] = {"--scene", "--width", "--seed", "--gpus", "--grid", "--out", "--png"};
+  for (int i = 1; i < argc; ++i) {
+    const bool valued = std::any_of(std::begin(kValued), std::end(kValued),
+                                    [&](const char* f) { return std::strcmp(argv[i], f) == 0; });
+    if (!valued) continue;
+    if (i + 1 >= argc) {
+      std::fprintf(stderr, "missing value for %s\n", argv[i]);
+      return 2;
+    }
     if (std::strcmp(argv[i], "--gpus") == 0) gpus_arg = std::atoi(argv[i + 1]);
+    ++i;
+  }
   std::thread prep([&] {
     const auto t = std::chrono::steady_clock::now();
     ndev = rt_device_count();   // the process's first HIP call: runtime start-up
@@ -65,13 +78,7 @@ int main(int argc, char** argv) {
   });
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
-    auto val = [&]() -> const char* {
-      if (i + 1 >= argc) {
-        std::fprintf(stderr, "missing value for %s\n", a.c_str());
-        std::exit(2);
-      }
-      return argv[++i];
-    };
+    auto val = [&]() -> const char* { return argv[++i]; };   // (present: checked above)
     if (a == "--scene") scene = val();
     else if (a == "--width") width = std::atoi(val());
     else if (a == "--seed") seed = std::strtoull(val(), nullptr, 10);

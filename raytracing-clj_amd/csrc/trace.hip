@@ -169,7 +169,11 @@ __device__ __forceinline__ float rng_centered(uint32_t& s) {
   s ^= s << 13;
   s ^= s >> 17;
   s ^= s << 5;
+#if RTCLJ_AB_RNGMUL
+  return static_cast<float>(s >> 8) * 0x1p-24f - 0.5f;
+#else
   return fmaf(static_cast<float>(s >> 8), 0x1p-24f, -0.5f);
+#endif
 }
 
 // rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32, so one fma
@@ -178,7 +182,11 @@ __device__ __forceinline__ float rng_sym(uint32_t& s) {
   s ^= s << 13;
   s ^= s >> 17;
   s ^= s << 5;
+#if RTCLJ_AB_RNGMUL
+  return static_cast<float>(s >> 8) * 0x1p-23f - 1.0f;
+#else
   return fmaf(static_cast<float>(s >> 8), 0x1p-23f, -1.0f);
+#endif
 }
 
 // stats builds: count one event per wave (by its first active lane)
@@ -330,6 +338,13 @@ struct alignas(16) Pair {
   f2 x, y, z, w;   // centres and -r^2 of bodies 2p and 2p+1
 };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// v_fma_f32 in its three-address (VOP3) form: the compiler's v_fmac_f32 needs
+// a v_mov copy when the addend stays live (a loop-invariant plane offset)
+__device__ __forceinline__ float fma3(float a, float b, float c) {
+  float r;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ f2 bc_lo(f2 v) { return __builtin_shufflevector(v, v, 0, 0); }
 __device__ __forceinline__ f2 bc_hi(f2 v) { return __builtin_shufflevector(v, v, 1, 1); }
 
@@ -388,6 +403,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   __shared__ int s_mb_post[4], s_mb_take[4], s_alive, s_mb_avail;
   // per wave: post when down to this many paths (0: posted once already; -1: off)
   __shared__ int s_mb_lim[4];
+#if RTCLJ_AB_CAMLDS
+  // the camera, laid out so the disk vectors and the centre read as float4s:
+  // [0] = centre, p00.x  [1] = p00.yz, du.xy  [2] = du.z, dv  [3] = disk_u, -  [4] = disk_v, -
+  __shared__ float4 s_cam[5];
+#endif
   // A/B build only (-DRTCLJ_AB_RING): camera samples made in
   // per-wave batches into LDS rings.  Worth 2.6 % at 5 workgroups per CU,
   // but its 5 KB of LDS keep the default traversal from the sixth (§8)
@@ -622,6 +642,14 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     s_mb_lim[threadIdx.x] = ka->compact > 0 ? ka->compact : -1;
   }
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0;
+#if RTCLJ_AB_CAMLDS
+  if (threadIdx.x < 20) {
+    const int t = static_cast<int>(threadIdx.x);
+    // words 0..11: centre, p00, du, dv; 12..15: disk_u, 0; 16..19: disk_v, 0
+    const int src = t < 12 ? t : (t & 3) == 3 ? -1 : t < 16 ? 12 + (t & 3) : 15 + (t & 3);
+    reinterpret_cast<float*>(s_cam)[t] = src >= 0 ? a.cam[src] : 0.0f;
+  }
+#endif
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
@@ -961,9 +989,18 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
       const float fx = fpx + rng_centered(st);
       const float fy = fgy + rng_centered(st);
+#if RTCLJ_AB_CAMLDS
+      // the camera from the workgroup's LDS copy: VGPR operands (an SGPR
+      // operand keeps a v_fma_f32 from dual-issuing)
+      const float4 cm0 = s_cam[0], cm1 = s_cam[1], cm2 = s_cam[2];
+      const float sx = fmaf(cm2.y, fy, fmaf(cm1.z, fx, cm0.w));
+      const float sy = fmaf(cm2.z, fy, fmaf(cm1.w, fx, cm1.x));
+      const float sz = fmaf(cm2.w, fy, fmaf(cm2.x, fx, cm1.y));
+#else
       const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
       const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
+#endif
       if (a.defocus) {
         // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
         float qx, qy2;
@@ -976,9 +1013,16 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           qy2 = rng_sym(st);
         } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
         if constexpr (STATS) st_fl += 12;
+#if RTCLJ_AB_CAMLDS
+        const float4 cm3 = s_cam[3], cm4 = s_cam[4], cm0 = s_cam[0];
+        ox = fmaf(cm4.x, qy2, fmaf(cm3.x, qx, cm0.x));
+        oy = fmaf(cm4.y, qy2, fmaf(cm3.y, qx, cm0.y));
+        oz = fmaf(cm4.z, qy2, fmaf(cm3.z, qx, cm0.z));
+#else
         ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
         oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
         oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
+#endif
       } else {
         ox = cx;
         oy = cy;
@@ -1262,12 +1306,21 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         f2 tnx, tfx, tny, tfy, tnz, tfz;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
+#if RTCLJ_AB_FMA3
+          tnx[e] = fma3(x0[e], r_xy.x, nf_x.x);
+          tfx[e] = fma3(x1[e], r_xy.x, nf_x.y);
+          tny[e] = fma3(y0[e], r_xy.y, nf_y.x);
+          tfy[e] = fma3(y1[e], r_xy.y, nf_y.y);
+          tnz[e] = fma3(z0[e], r_z.x, nf_z.x);
+          tfz[e] = fma3(z1[e], r_z.x, nf_z.y);
+#else
           tnx[e] = fmaf(x0[e], r_xy.x, nf_x.x);
           tfx[e] = fmaf(x1[e], r_xy.x, nf_x.y);
           tny[e] = fmaf(y0[e], r_xy.y, nf_y.x);
           tfy[e] = fmaf(y1[e], r_xy.y, nf_y.y);
           tnz[e] = fmaf(z0[e], r_z.x, nf_z.x);
           tfz[e] = fmaf(z1[e], r_z.x, nf_z.y);
+#endif
         }
         tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
@@ -2668,8 +2721,11 @@ struct Schedule {
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
   ScheduleKey key{};
-  unsigned long long* part = nullptr;   // [split][rows][width][3] pixel sums of split tiles
+  unsigned long long* part = nullptr;   // [rows][width][3] pixel sums of split tiles (zero between launches)
   size_t part_cap = 0;                  // u64 elements
+  // a split launch's trace kernel was enqueued but its finalize_kernel (which
+  // re-zeroes the sums) was not: the next split launch zeroes them first
+  bool part_dirty = false;
   // the stealing state (KArgs word, done, sum, owner, stealc)
   unsigned long long* word = nullptr;   // per tile
   unsigned* done = nullptr;             // per tile
@@ -2732,30 +2788,34 @@ struct rt_dscene {
   float4* mat;
   int* kind;
   bool unit_albedo;            // every lambertian/metal albedo channel within [-1, 1] (compact_ok)
+  uint64_t uid;                // upload id (scene_uid): contexts name scenes by it, not by address
   mutable ScheduleSet sched;   // rt_launch's adaptive tile order
 };
+static std::atomic<uint64_t> g_scene_uid{0};
+uint64_t rtclj::scene_uid(const rt_dscene* ds) { return ds ? ds->uid : 0; }
 
 // live device scenes, for release_stream_schedules (rt_host.cpp's contexts)
 static std::mutex g_scenes_mu;
 static std::vector<rt_dscene*> g_scenes;
 
-// the live scenes among `scenes` (a context's list may name freed ones)
+// the live scenes among `uids` (a context's list may name freed ones; a
+// new scene at a freed one's address has another id)
 template <class F>
-static void for_live_scenes(const void* const* scenes, int n, F f) {
+static void for_live_scenes(const uint64_t* uids, int n, F f) {
   std::lock_guard<std::mutex> lk(g_scenes_mu);
   for (rt_dscene* d : g_scenes)
-    if (std::find(scenes, scenes + n, static_cast<const void*>(d)) != scenes + n) {
+    if (std::find(uids, uids + n, d->uid) != uids + n) {
       std::lock_guard<std::mutex> l2(d->sched.mu);
       f(d->sched);
     }
 }
 
-void rtclj::release_stream_schedules(void* stream, const void* const* scenes, int n) {
-  for_live_scenes(scenes, n, [&](ScheduleSet& set) { set.release_stream(static_cast<hipStream_t>(stream)); });
+void rtclj::release_stream_schedules(void* stream, const uint64_t* uids, int n) {
+  for_live_scenes(uids, n, [&](ScheduleSet& set) { set.release_stream(static_cast<hipStream_t>(stream)); });
 }
 
-void rtclj::rebind_stream_schedules(void* from, void* to, const void* const* scenes, int n) {
-  for_live_scenes(scenes, n, [&](ScheduleSet& set) {
+void rtclj::rebind_stream_schedules(void* from, void* to, const uint64_t* uids, int n) {
+  for_live_scenes(uids, n, [&](ScheduleSet& set) {
     Schedule* src = nullptr;
     for (int k = 0; k < set.used; ++k) {
       if (set.s[k].stream == static_cast<hipStream_t>(to)) return;
@@ -2847,6 +2907,7 @@ extern "C" int rt_scene_upload(int device, const rt_scene* s, rt_dscene** out) {
     o[4] = b0.z; o[5] = b1.z; o[6] = b0.w; o[7] = b1.w;
   }
   rt_dscene* d = new rt_dscene{};
+  d->uid = ++g_scene_uid;
   d->device = device;
   d->n = n;
   d->n_pad = n_pad;
@@ -2994,8 +3055,11 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
 // 22 too); elsewhere the launch runs 16.  Seven workgroups per CU instead of
 // six, in 72 VGPRs without a spill: C1 5.90 -> 5.83 ms (profiles/r04/w7/,
 // DESIGN.md §8.1).
+// Its pixel table packs a pixel's image coordinates as x | y << 16: frames
+// up to 65536 pixels wide and high (wider or taller ones run 16).
 static bool compact_ok(const rt_dscene& ds, const rt_params& p) {
-  return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp <= 255 && ds.tree[1].depth + 2 <= kBvhStack;
+  return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp <= 255 && ds.tree[1].depth + 2 <= kBvhStack &&
+         p.width <= 65536 && p.height <= 65536;
 }
 static int launch_variant(const rt_dscene& ds, const rt_params& p) {
   const int sel = g_variant.load();
@@ -3270,6 +3334,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMalloc(&sch->part, need * sizeof(unsigned long long)));
       HIP_TRY(hipMemsetAsync(sch->part, 0, need * sizeof(unsigned long long), stream));
       sch->part_cap = need;
+      sch->part_dirty = false;
+    }
+    if (sch->part_dirty) {   // an earlier launch failed between its trace and finalize kernels
+      HIP_TRY(hipMemsetAsync(sch->part, 0, sch->part_cap * sizeof(unsigned long long), stream));
+      sch->part_dirty = false;
     }
     a.part = sch->part;
   }
@@ -3415,6 +3484,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // profiles/r04/lds_batch/)
   a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 256, 64));
   void* args[] = {&a};
+  if (split > 1) sch->part_dirty = true;   // (cleared once finalize_kernel is enqueued)
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
   if (split > 1) {
     unsigned long long* part = a.part;
@@ -3424,6 +3494,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     void* fargs[] = {&part, &order, &nw, &tx, &tht, &w, &nr, &out, &spp, &realm};
     HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&finalize_kernel), dim3(n_tiles - n_whole), dim3(kTile * 3 * th),
                             fargs, 0, stream));
+    sch->part_dirty = false;
   }
   if (a.tile_cost) {
     // the next launch's order, stream-ordered after this kernel (no host sync)

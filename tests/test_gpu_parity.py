@@ -537,7 +537,7 @@ def test_compact_variant_limits(gpu_lib):
     where a u32 sum cannot overflow: spp <= 255 and every albedo within
     [-1, 1]. At spp 255 -- the largest sums -- it equals the mirror bit for
     bit; at 256, or with an albedo above 1, the launch runs 16 (u64 sums).
-    The default selector keeps 16."""
+    The default selector runs 22 wherever it applies."""
     import ctypes as C
     from rtclj import raytracing as R
     from rtclj import scenes
@@ -570,3 +570,33 @@ def test_compact_variant_limits(gpu_lib):
         g = R.render(sc, cam, 160, 90, spp=255, seed=3)
     ref, _, _ = _mirror(sc, cam, 160, 90, 255, 50, seed=3)
     assert np.array_equal(g, ref)
+
+
+def test_compact_variant_wide_frame(gpu_lib):
+    """Variant 22's pixel table packs (x | y << 16): a frame wider than 65536
+    pixels runs 16 instead, and its columns past 65536 equal the
+    mirror bit for bit (a 70000 x 2 frame at 1 spp, those columns checked)."""
+    import ctypes as C
+    from rtclj import raytracing as R
+    from rtclj import scenes
+    from rtclj._lib import check, lib, rt_params
+    sc = scenes.cover(11)
+    w, h = 70000, 2
+    ds = C.c_void_p()
+    check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    try:
+        o = (C.c_int * 4)()
+        p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=1, max_depth=50, seed=1)
+        check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+        assert o[3] == 16, o[3]
+        p = rt_params(width=65536, height=h, row_begin=0, row_end=h, spp=1, max_depth=50, seed=1)
+        check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+        assert o[3] == 22, o[3]
+    finally:
+        lib.rt_scene_free(ds)
+    cam = scenes.cover_camera(w, h)
+    g = R.render(sc, cam, w, h, spp=1, seed=5)
+    cols = (65520, 65600)
+    ref, _, _, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+                                 sc.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, 1, 50, seed=5, cols=cols)
+    assert np.array_equal(g[:, cols[0]:cols[1]], ref[:, cols[0]:cols[1]])
