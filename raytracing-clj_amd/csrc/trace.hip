@@ -169,11 +169,7 @@ __device__ __forceinline__ float rng_centered(uint32_t& s) {
   s ^= s << 13;
   s ^= s >> 17;
   s ^= s << 5;
-#if RTCLJ_AB_RNGMUL
-  return static_cast<float>(s >> 8) * 0x1p-24f - 0.5f;
-#else
   return fmaf(static_cast<float>(s >> 8), 0x1p-24f, -0.5f);
-#endif
 }
 
 // rand-double -1 1 = -1 + 2*xi (vec3a.clj:71-72): exact in fp32, so one fma
@@ -182,11 +178,7 @@ __device__ __forceinline__ float rng_sym(uint32_t& s) {
   s ^= s << 13;
   s ^= s >> 17;
   s ^= s << 5;
-#if RTCLJ_AB_RNGMUL
-  return static_cast<float>(s >> 8) * 0x1p-23f - 1.0f;
-#else
   return fmaf(static_cast<float>(s >> 8), 0x1p-23f, -1.0f);
-#endif
 }
 
 // stats builds: count one event per wave (by its first active lane)
@@ -332,6 +324,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // LDS (address space 3) pointers: 32-bit addresses, ds_read with immediate offsets
 typedef const char __attribute__((address_space(3)))* LdsC;
 typedef const f2 __attribute__((address_space(3)))* LdsF2;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const f4v __attribute__((address_space(3)))* LdsF4;
 typedef const long long __attribute__((address_space(3)))* LdsI64;
 __device__ __forceinline__ unsigned lds_addr(const void* p) { return static_cast<unsigned>((uintptr_t)(LdsC)p); }
 struct alignas(16) Pair {
@@ -403,11 +397,6 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   __shared__ int s_mb_post[4], s_mb_take[4], s_alive, s_mb_avail;
   // per wave: post when down to this many paths (0: posted once already; -1: off)
   __shared__ int s_mb_lim[4];
-#if RTCLJ_AB_CAMLDS
-  // the camera, laid out so the disk vectors and the centre read as float4s:
-  // [0] = centre, p00.x  [1] = p00.yz, du.xy  [2] = du.z, dv  [3] = disk_u, -  [4] = disk_v, -
-  __shared__ float4 s_cam[5];
-#endif
   // A/B build only (-DRTCLJ_AB_RING): camera samples made in
   // per-wave batches into LDS rings.  Worth 2.6 % at 5 workgroups per CU,
   // but its 5 KB of LDS keep the default traversal from the sixth (§8)
@@ -507,10 +496,10 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // child refs at ref + 72 and its planes at ref + the ray's plane
       // offsets, with no base added (float4 4 of each 80-byte node holds
       // c0, c1 in .z, .w; leaf refs are negative and stay)
-      // The leaves are laid out as records: a leaf's two pairs (64 B) and
-      // their body indices (16 B) side by side, 80 B, so a leaf pass reads
-      // everything from one address; a leaf ref ~p (p = its first pair, even)
-      // becomes ~(the record's LDS address).
+      // The leaves are laid out as records: a leaf's four bodies as float4s
+      // (cx, cy, cz, -r^2) and their indices (16 B) side by side, 80 B, so a
+      // leaf pass and its exact passes read everything from one address; a
+      // leaf ref ~p (p = its first pair, even) becomes ~(the record's LDS address).
       const int nb0 = static_cast<int>(lds_addr(s_geo));
       const int nodes_f4 = a.bvh_off_pairs >> 4;
       const int pairs_f4 = (a.bvh_off_pidx - a.bvh_off_pairs) >> 4;   // 2 per pair
@@ -528,7 +517,13 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           }
         } else if (i < nodes_f4 + pairs_f4) {   // pair k / 2, half k % 2
           const int k = i - nodes_f4, pr = k >> 1;
-          d = nodes_f4 + (pr >> 1) * 5 + (pr & 1) * 2 + (k & 1);
+          // (per-body float4s: half 0 holds the pair's x and y, half 1 z and w)
+          float* rb = reinterpret_cast<float*>(s_geo) + 4 * (nodes_f4 + (pr >> 1) * 5 + (pr & 1) * 2) + 2 * (k & 1);
+          rb[0] = v.x;
+          rb[4] = v.y;
+          rb[1] = v.z;
+          rb[5] = v.w;
+          continue;
         } else {                                 // the indices of pairs 2k, 2k + 1
           d = nodes_f4 + (i - nodes_f4 - pairs_f4) * 5 + 4;
         }
@@ -642,14 +637,6 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     s_mb_lim[threadIdx.x] = ka->compact > 0 ? ka->compact : -1;
   }
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0;
-#if RTCLJ_AB_CAMLDS
-  if (threadIdx.x < 20) {
-    const int t = static_cast<int>(threadIdx.x);
-    // words 0..11: centre, p00, du, dv; 12..15: disk_u, 0; 16..19: disk_v, 0
-    const int src = t < 12 ? t : (t & 3) == 3 ? -1 : t < 16 ? 12 + (t & 3) : 15 + (t & 3);
-    reinterpret_cast<float*>(s_cam)[t] = src >= 0 ? a.cam[src] : 0.0f;
-  }
-#endif
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
@@ -989,18 +976,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // xi - 0.5 is exact in fp32: one fma of the 24-bit integer, the same bits
       const float fx = fpx + rng_centered(st);
       const float fy = fgy + rng_centered(st);
-#if RTCLJ_AB_CAMLDS
-      // the camera from the workgroup's LDS copy: VGPR operands (an SGPR
-      // operand keeps a v_fma_f32 from dual-issuing)
-      const float4 cm0 = s_cam[0], cm1 = s_cam[1], cm2 = s_cam[2];
-      const float sx = fmaf(cm2.y, fy, fmaf(cm1.z, fx, cm0.w));
-      const float sy = fmaf(cm2.z, fy, fmaf(cm1.w, fx, cm1.x));
-      const float sz = fmaf(cm2.w, fy, fmaf(cm2.x, fx, cm1.y));
-#else
       const float sx = fmaf(a.cam[9], fy, fmaf(a.cam[6], fx, a.cam[3]));
       const float sy = fmaf(a.cam[10], fy, fmaf(a.cam[7], fx, a.cam[4]));
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
-#endif
       if (a.defocus) {
         // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
         float qx, qy2;
@@ -1013,16 +991,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           qy2 = rng_sym(st);
         } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
         if constexpr (STATS) st_fl += 12;
-#if RTCLJ_AB_CAMLDS
-        const float4 cm3 = s_cam[3], cm4 = s_cam[4], cm0 = s_cam[0];
-        ox = fmaf(cm4.x, qy2, fmaf(cm3.x, qx, cm0.x));
-        oy = fmaf(cm4.y, qy2, fmaf(cm3.y, qx, cm0.y));
-        oz = fmaf(cm4.z, qy2, fmaf(cm3.z, qx, cm0.z));
-#else
         ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
         oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
         oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
-#endif
       } else {
         ox = cx;
         oy = cy;
@@ -1170,11 +1141,54 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           const uint64_t ex = __builtin_amdgcn_read_exec();
           if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_leafw;
         }
-        // an 8-body leaf runs as two 4-body halves, each with its own exact
+        // (the other trees: pairs and their indices in separate arrays; an
+        // 8-body leaf runs as two 4-body halves, each with its own exact
         // passes: 4 bodies' (h, disc, index) live at a time, not 8 (103 -> ~90
-        // VGPRs, 4 -> 5 waves per SIMD); the acceptance is order-independent
+        // VGPRs, 4 -> 5 waves per SIMD); the acceptance is order-independent)
         constexpr int NPL = leaf_pairs(SCAN);
         constexpr int NP = NPL > 2 ? 2 : NPL;   // pairs per half
+        if constexpr (kLeafRec) {
+          // The 4-body record holds each body as a float4 (cx, cy, cz, -r^2) at
+          // + 16 j and the four indices at + 64.  The leaf pass keeps only the
+          // candidate mask; an exact pass re-reads its body (address + 2k for
+          // mask bit k = 8 j) and recomputes (h, disc) with the same ops --
+          // the same bits -- instead of selecting them from 12 live registers
+          // with compares and v_cndmask (single-port instructions).
+          unsigned pa = static_cast<unsigned>(p);
+          asm volatile("" : "+v"(pa));
+          auto body = [&](unsigned addr, float& h, float& c, float& disc) {
+            const f4v g = *(LdsF4)(uintptr_t)addr;
+            const float ocx = g.x - o_xy.x, ocy = g.y - o_xy.y, ocz = g.z - o_zux.x;
+            h = fmaf(u_yz.y, ocz, fmaf(u_yz.x, ocy, o_zux.y * ocx));
+            c = fmaf(ocx, ocx, fmaf(ocz, ocz, fmaf(ocy, ocy, g.w)));
+            disc = fmaf(h, h, -c);
+          };
+          asm volatile("" : "+v"(o_xy), "+v"(o_zux), "+v"(u_yz));
+          unsigned nc[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (STATS) st_fl += 16;
+            float h, c, disc;
+            body(pa + 16u * j, h, c, disc);
+            nc[j] = __builtin_amdgcn_bitop3_b32(__float_as_uint(disc), __float_as_uint(h), __float_as_uint(c), 0x0b);
+          }
+          const unsigned b01 = __builtin_amdgcn_perm(nc[1], nc[0], 0x0c0c0b09u);
+          const unsigned b23 = __builtin_amdgcn_perm(nc[3], nc[2], 0x0b090c0cu);
+          unsigned m = __builtin_amdgcn_bitop3_b32(b01, b23, 0x01010101u, 0xa8);
+          while (m) {
+            if constexpr (STATS) {
+              const uint64_t ex = __builtin_amdgcn_read_exec();
+              if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_consw;
+            }
+            const unsigned k = __builtin_ctz(m);
+            m &= m - 1;
+            float h, c, disc;
+            body(pa + k + k, h, c, disc);
+            const int sidx = *(const int __attribute__((address_space(3)))*)(uintptr_t)(pa + 64u + (k >> 1));
+            consider_tie(h, disc, sidx);
+          }
+          return;
+        }
 #pragma unroll
         for (int hb = 0; hb < NPL; hb += NP) {
         float hh[2 * NP], dd[2 * NP];
@@ -1184,26 +1198,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         // rest; indexing p + 1 let the compiler rebuild it as -c, a 2nd base)
         const Pair* const lp = pairs + p;
         const PidxT* const li = pidx + p;
-        // (a leaf record's address opaque: its reads are immediate offsets
-        // from it, not (k - 1) - c rebuilt from the ref c = ~address per read)
-        unsigned pa = static_cast<unsigned>(p);
-        if constexpr (kLeafRec) asm volatile("" : "+v"(pa));
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
           if constexpr (STATS) st_fl += 32;   // 2 bodies x (oc 3, h 5, c 6, disc 2)
-          Pair g;
-          PidxT id;
-          if constexpr (kLeafRec) {
-            // p is the leaf record's LDS address: pair q at + 32 q, its
-            // indices at + 64 + 8 q (immediate offsets of one address)
-            const LdsF2 lg = (LdsF2)(uintptr_t)(pa + 32u * (hb + q));
-            g.x = lg[0], g.y = lg[1], g.z = lg[2], g.w = lg[3];
-            const long long i2 = *(LdsI64)(uintptr_t)(pa + 64u + 8u * (hb + q));
-            id = PidxT{static_cast<int>(i2), static_cast<int>(i2 >> 32)};
-          } else {
-            g = lp[hb + q];
-            id = li[hb + q];
-          }
+          const Pair g = lp[hb + q];
+          const PidxT id = li[hb + q];
           asm volatile("" : "+v"(o_xy), "+v"(o_zux), "+v"(u_yz));
           // (scalar fp32 per body, not v_pk_*: a packed op issues on one VALU
           // port only, two v_fma_f32 dual-issue -- 5.84 -> 5.45 ms on C1
@@ -1273,8 +1272,8 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // bound only makes the test pass: conservative)
       // (the near plane's t is the min of the two planes' t, bit for bit: the
       // same fma on the same operands -- no min/max orders them)
-      auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
-        if constexpr (STATS) st_fl += 24;   // 6 packed fma over 2 children
+      auto node_planes = [&](int node, float& tn0, float& tn1, float& tf0, float& tf1, int& c0, int& c1) {
+        if constexpr (STATS) st_fl += 24;   // 12 fma over 2 children
         // node * 80 as a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
         // the 4-body tree's inner-child refs are byte offsets (node * 80,
         // written by rt_scene_upload): no multiply per step
@@ -1306,26 +1305,23 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         f2 tnx, tfx, tny, tfy, tnz, tfz;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-#if RTCLJ_AB_FMA3
           tnx[e] = fma3(x0[e], r_xy.x, nf_x.x);
           tfx[e] = fma3(x1[e], r_xy.x, nf_x.y);
           tny[e] = fma3(y0[e], r_xy.y, nf_y.x);
           tfy[e] = fma3(y1[e], r_xy.y, nf_y.y);
           tnz[e] = fma3(z0[e], r_z.x, nf_z.x);
           tfz[e] = fma3(z1[e], r_z.x, nf_z.y);
-#else
-          tnx[e] = fmaf(x0[e], r_xy.x, nf_x.x);
-          tfx[e] = fmaf(x1[e], r_xy.x, nf_x.y);
-          tny[e] = fmaf(y0[e], r_xy.y, nf_y.x);
-          tfy[e] = fmaf(y1[e], r_xy.y, nf_y.y);
-          tnz[e] = fmaf(z0[e], r_z.x, nf_z.x);
-          tfz[e] = fmaf(z1[e], r_z.x, nf_z.y);
-#endif
         }
         tn0 = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
         tn1 = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
-        const float tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
-        const float tf1 = fminf(fminf(tfx.y, tfy.y), tfz.y);
+        tf0 = fminf(fminf(tfx.x, tfy.x), tfz.x);
+        tf1 = fminf(fminf(tfx.y, tfy.y), tfz.y);
+        c0 = ch.x;
+        c1 = ch.y;
+      };
+      auto node_test = [&](int node, float& tn0, float& tn1, bool& hit0, bool& hit1, int& c0, int& c1) {
+        float tf0, tf1;
+        node_planes(node, tn0, tn1, tf0, tf1, c0, c1);
         // "[tn, tf] meets (tmin, best_t]" as max(tn, tmin) <= min(tf, best_t),
         // spelled tn <= min(tf, best_t) and tmin <= tf (tmin < best_t always):
         // a compare instead of a max per child.  Each is "not greater", so a
@@ -1337,8 +1333,6 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         asm("v_min_f32 %0, %1, %2" : "=v"(tb1) : "v"(tf1), "v"(best_t));
         hit0 = !(tn0 > tb0) & !(tmin > tf0);
         hit1 = !(tn1 > tb1) & !(tmin > tf1);
-        c0 = ch.x;
-        c1 = ch.y;
       };
       // the big bodies' leaves first: every lane, so a wave-uniform loop (their
       // hits, e.g. the ground, then cull the tree)

@@ -22,8 +22,12 @@ def classify(line):
     if base in TRANS:
         return "T"
     if base in DUAL:
-        # an SGPR or (non-inline) operand makes v_fma single-port (measured)
-        if base in ("v_fma_f32",) and re.search(r",\s*s\d+|,\s*s\[", line):
+        # any SGPR source operand makes an instruction single-port (measured:
+        # v_fma/add/mul/sub_f32, v_add_u32, v_xor, v_bitop3 with an SGPR
+        # operand all take a whole quad-cycle; inline constants and literals do not)
+        ops = line.split(";")[0].split(None, 1)[1] if len(line.split(None, 1)) > 1 else ""
+        srcs = ops.split(",")[1:]
+        if any(re.match(r"\s*-?\|?(s\d+|s\[|vcc|exec)", x) for x in srcs):
             return "S"
         return "D"
     if base.startswith("v_readlane") or base.startswith("v_writelane") or base.startswith("v_readfirstlane"):
@@ -33,7 +37,8 @@ def classify(line):
 
 def main():
     lines = open(sys.argv[1]).read().split("\n")
-    for rng in sys.argv[2:]:
+    verbose = "-v" in sys.argv
+    for rng in [x for x in sys.argv[2:] if x != "-v"]:
         a, b = (int(x) for x in rng.split(":"))
         c = {"D": 0, "S": 0, "T": 0}
         salu = 0
@@ -41,6 +46,8 @@ def main():
             k = classify(ln)
             if k:
                 c[k] += 1
+                if verbose and k != "D":
+                    print(f"      {k} {ln.strip()}")
             elif re.match(r"\s+s_", ln):
                 salu += 1
         q = c["D"] * 0.5 + c["S"] + 2 * c["T"]

@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 #define V8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
@@ -85,6 +86,13 @@ __device__ __forceinline__ void op8(float (&r)[8], float a, float b) {
   if constexpr (OP == 91) asm volatile("v_min_u32 %0, %0, %1" : "+v"(r[i]) : "v"(a)); \
   if constexpr (OP == 92) asm volatile("v_max_i32 %0, %0, %1" : "+v"(r[i]) : "v"(a)); \
   if constexpr (OP == 93) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(a), "v"(b)); \
+  if constexpr (OP == 96) asm volatile("v_add_f32_e64 %0, %0, %2" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 97) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xb" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 98) asm volatile("v_mul_f32_e64 %0, %0, %2" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 99) asm volatile("v_add_u32_e64 %0, %0, %2" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 100) asm volatile("v_xor_b32_e64 %0, %0, %2" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 101) asm volatile("v_fma_f32 %0, %0, %1, 2.0" : "+v"(r[i]) : "v"(a), "s"(b)); \
+  if constexpr (OP == 102) asm volatile("v_sub_f32_e64 %0, %2, %0" : "+v"(r[i]) : "v"(a), "s"(b)); \
   if constexpr (OP == 65) { if (i & 1) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[60:61]" : "+v"(r[i]) : "v"(a)); else asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(r[i]) : "v"(a), "v"(b)); }
   V8(ONE)
 #undef ONE
@@ -205,6 +213,14 @@ static const char* name(int op) {
     case 67: return "fma / cndmask_e32 (vcc) alternating";
     case 68: return "cmp_e64 + cndmask_e64 (2 sgpr pairs)";
     case 69: return "v_cndmask_e32 (vcc from v_cmp)";
+    case 96: return "v_add_f32 (sgpr operand)";
+    case 97: return "v_bitop3_b32 (sgpr operand)";
+    case 98: return "v_mul_f32 (sgpr operand)";
+    case 99: return "v_add_u32 (sgpr operand)";
+    case 100: return "v_xor_b32 (sgpr operand)";
+    case 101: return "v_fma_f32 (inline const)";
+    case 102: return "v_sub_f32 (sgpr operand)";
+
     case 70: return "v_alignbit_b32";
     case 71: return "v_lshlrev_b32 (vgpr amount)";
     case 72: return "v_bfe_u32";
@@ -280,6 +296,14 @@ int main() {
   printf("# %s, %d CUs: cycles per wave64 instruction per SIMD (8 independent chains)\n", p.gcnArchName, cus);
   run<0>(d, clk, cus);
   run<0>(d, clk, cus);
+  run<96>(d, clk, cus);
+  run<97>(d, clk, cus);
+  run<98>(d, clk, cus);
+  run<99>(d, clk, cus);
+  run<100>(d, clk, cus);
+  run<101>(d, clk, cus);
+  run<102>(d, clk, cus);
+  if (getenv("VALU_COST_NEW_ONLY")) return 0;
   run<1>(d, clk, cus);
   run<2>(d, clk, cus);
   run<3>(d, clk, cus);
