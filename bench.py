@@ -61,7 +61,7 @@ def metric_for(width, height, spp, depth):
     return f"Mray-samples/sec at {width}×{height}×{spp}spp depth{depth}; achieved HBM GB/s vs peak"
 
 # committed rocprofv3 PMC passes of the current build (profiles/pmc.sh), per workload
-PMC_DIRS = {"c1": ROOT / "profiles" / "r04" / "pmc_c1", "c4": ROOT / "profiles" / "r04" / "pmc_c4"}
+PMC_DIRS = {"c1": ROOT / "profiles" / "r05" / "pmc_c1", "c4": ROOT / "profiles" / "r05" / "pmc_c4"}
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -284,20 +284,45 @@ def pmc_traffic(pmc_dir):
 
 
 def pmc_valu(pmc_dir, n_simd=1024, n_xcd=8):
-    """VALU issue picture of the same launches: issue_busy = fraction of
-    4-cycle slots in which a SIMD issues a VALU instruction
-    (SQ_ACTIVE_INST_VALU x 4 / SIMDs vs GRBM_GUI_ACTIVE / XCDs); lanes_active
-    = mean fraction of the 64 lanes active per VALU instruction."""
-    v = _pmc_avg(pmc_dir, ("insts", "waves"), ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU",
-                                      "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES"))
-    if v is None:
+    """VALU issue picture of the same launches (profiles/pmc.sh passes valu1,
+    valu2, waits).  On gfx950 a SIMD issues up to two VALU
+    instructions per quad-cycle (4 shader cycles): the full-rate ops (fp32
+    fma/add/mul, 32-bit add/logic, v_mov, right shifts) dual-issue, the rest
+    (packed and 64-bit ops, compares, selects, conversions, min/max, left
+    shifts, and ANY instruction with an SGPR operand) take a quad-cycle of
+    their own, transcendentals two (measured: profiles/r05/valu/).
+      valu_busy       = quad-cycles with >= 1 VALU issue / SIMD quad-cycles
+                      = (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (SIMDs x cycles / 4)
+      dual_issue      = SQ_ACTIVE_INST_VALU2 / those busy quad-cycles
+      valu_pipe_util  = SQ_INSTS_VALU x 2 / (SIMDs x cycles): the pipe as if every
+                        instruction took 2 cycles (a lower bound: single-port ops take 4)
+      lanes_active    = SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU / 64
+      salu_per_valu   = SQ_INSTS_SALU / SQ_INSTS_VALU
+      wait_dep, wait_issue, issuing = SQ_WAIT_ANY, SQ_WAIT_INST_ANY,
+                        SQ_ACTIVE_INST_ANY as shares of SQ_WAVE_CYCLES (wave residency)."""
+    v1 = _pmc_avg(pmc_dir, ("valu1",), ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU",
+                                        "SQ_THREAD_CYCLES_VALU", "GRBM_GUI_ACTIVE"))
+    v2 = _pmc_avg(pmc_dir, ("valu2",), ("SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "GRBM_GUI_ACTIVE"))
+    v3 = _pmc_avg(pmc_dir, ("waits",), ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                        "GRBM_GUI_ACTIVE"))
+    if v1 is None:
         return None
-    busy = v["SQ_ACTIVE_INST_VALU"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd)
-    lanes = v["SQ_THREAD_CYCLES_VALU"] / v["SQ_INSTS_VALU"] / 64.0
-    return {"issue_busy": busy, "lanes_active": lanes, "issue_utilisation": busy * lanes,
-            "valu_insts": v["SQ_INSTS_VALU"],
-            "mean_waves_per_simd": v["SQ_WAVE_CYCLES"] * 4.0 / n_simd / (v["GRBM_GUI_ACTIVE"] / n_xcd),
-            "source": str(pmc_dir.relative_to(ROOT))}
+    cyc = v1["GRBM_GUI_ACTIVE"] / n_xcd
+    quads = n_simd * cyc / 4.0
+    busy_q = v1["SQ_ACTIVE_INST_VALU"] - v1["SQ_ACTIVE_INST_VALU2"]
+    out = {"valu_busy": busy_q / quads, "dual_issue": v1["SQ_ACTIVE_INST_VALU2"] / busy_q,
+           "valu_pipe_util": v1["SQ_INSTS_VALU"] * 2.0 / (n_simd * cyc),
+           "lanes_active": v1["SQ_THREAD_CYCLES_VALU"] / v1["SQ_INSTS_VALU"] / 64.0,
+           "valu_insts": v1["SQ_INSTS_VALU"], "source": str(pmc_dir.relative_to(ROOT))}
+    if v2 is not None:
+        out["salu_per_valu"] = v2["SQ_INSTS_SALU"] / v1["SQ_INSTS_VALU"]
+        out["branch_per_valu"] = v2["SQ_INSTS_BRANCH"] / v1["SQ_INSTS_VALU"]
+    if v3 is not None:
+        wc = v3["SQ_WAVE_CYCLES"]
+        out.update(wait_dep=v3["SQ_WAIT_ANY"] / wc, wait_issue=v3["SQ_WAIT_INST_ANY"] / wc,
+                   issuing=v3["SQ_ACTIVE_INST_ANY"] / wc,
+                   mean_waves_per_simd=wc * 4.0 / n_simd / (v3["GRBM_GUI_ACTIVE"] / n_xcd))
+    return out
 
 
 def occupancy(ds, p):
@@ -659,12 +684,16 @@ def main():
                                      f"statistics build (variant {stats['stats_variant']}, lib/librtclj_diag.so) of "
                                      f"the same frame")
         if valu is not None:
-            roof.update(issue_busy=valu["issue_busy"], lanes_active=valu["lanes_active"],
-                        issue_utilisation=valu["issue_utilisation"])
+            roof.update({k: valu[k] for k in ("valu_busy", "dual_issue", "valu_pipe_util", "lanes_active",
+                                              "salu_per_valu", "wait_dep", "wait_issue", "issuing") if k in valu})
         roof["note"] = ("VALU-issue bound: branchy per-ray fp32 work, no GEMM shape (MFMA unused), HBM not binding "
-                        "(hbm_roofline). peak = the packed fp32 vector rate. issue_utilisation = issue_busy x "
-                        "lanes_active (PMC): the SIMDs issue a VALU instruction in nearly every slot, and "
-                        "lanes_active of the 64 lanes do work in it.")
+                        "(hbm_roofline). peak = the fp32 vector rate (157.3 TF/s: 2 flops x 32 lanes per cycle per "
+                        "SIMD, i.e. v_fma_f32 dual-issued). PMC of the same launch: valu_busy = share of SIMD "
+                        "quad-cycles issuing a VALU instruction, dual_issue = share of those issuing two; "
+                        "single-port instructions (compares, selects, conversions, min/max, packed ops, SGPR "
+                        "operands) take a quad-cycle alone, so the pipe is full while frac stays low -- "
+                        "lanes_active of the 64 lanes do work per instruction (divergence). valu_pipe_util = "
+                        "SQ_INSTS_VALU x 2 / SIMD cycles assumes every instruction dual-issues (a lower bound).")
         roof["brute_force_equivalent"] = {
             "tflops": bf_tflops, "frac": bf_tflops / PEAK_FP32_TFLOPS,
             "note": f"SURVEY.md §8d's formula (17 x {len(scene)} bodies + 100 per segment) prices the linear scan; "

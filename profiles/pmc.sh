@@ -21,7 +21,7 @@ pass() {
   case $rc in 124|134|137|139) echo "stopping: GPU step failed ($rc)"; exit $rc ;; esac
   return 0
 }
-PASSES=${PMC_PASSES:-"waves insts lds sched fetch write"}
+PASSES=${PMC_PASSES:-"valu1 valu2 waits fetch write"}
 for g in $PASSES; do
   case $g in
     waves) pass waves SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE ;;

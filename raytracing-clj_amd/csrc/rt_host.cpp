@@ -567,7 +567,7 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, 
     return;
   }
   const auto t_enq = Clock::now();
-  if (e == hipSuccess) e = hipMemsetAsync(cx->d_cnt, 0, 2 * sizeof(uint64_t), cx->stream);
+  if (e == hipSuccess) e = static_cast<hipError_t>(fill_async(cx->d_cnt, 0, 2 * sizeof(uint64_t), cx->stream));
   if (e == hipSuccess) e = hipEventRecord(cx->e0, cx->stream);
   if (e != hipSuccess) {
     hip_fail(e, "rt_render setup");

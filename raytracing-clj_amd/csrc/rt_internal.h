@@ -56,6 +56,11 @@ uint64_t scene_uid(const rt_dscene* ds);
 // (no comparison holds).  Built once from rt_quantize's own arithmetic
 // (rt_host.cpp); the device quantiser (trace.hip) searches it.
 const float* quantize_thresholds();
+// Enqueue the library's fill kernel (trace.hip): `bytes` (a multiple of 4)
+// of p set to byte_value, on `stream` -- in place of hipMemsetAsync, whose
+// runtime blit kernel a fresh process would load on its first frame.
+// Returns the launch's hipError_t (0: enqueued).
+int fill_async(void* p, int byte_value, size_t bytes, void* stream);
 // Enqueue the device quantiser: d_out[i] = rt_quantize's byte of d_lin[i].
 // Returns the launch's hipError_t (0: enqueued).
 int quantize_launch(const float* d_lin, uint8_t* d_out, size_t n, void* stream);

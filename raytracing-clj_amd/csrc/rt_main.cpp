@@ -4,14 +4,16 @@
 // --realm mirrors `clojure -M:realm` (src/realm/raytracing.clj:279-359)
 // instead: realm's body order, camera (no defocus, focal length
 // |look-from - look-at|), height (int (/ ^double 400 ^double 16/9)) = 224 and
-// RT_FLAG_REALM semantics; it writes scene-realm.ppm.  --png also writes the
-// frame as a PNG (rt_write_png; what src/ppm2png.clj produces).  The frame
+// RT_FLAG_REALM semantics; it writes scene-realm.ppm.  Like the reference's
+// -main, whose (time ...) ends with (ppm->png "scene.ppm" "scene.png")
+// (raytracing.clj:176), it then converts the PPM it wrote to a PNG beside it
+// (rt_ppm_to_png; --png PATH names it, --no-png skips it), inside the timing.  The frame
 // is quantised on the device (rt_render_u8: a quarter of the copy back, no
 // host pass); --host-quantize takes rt_render's floats and rt_quantize
 // instead (the same bytes).
 //
 //   rt_main [spp] [depth] [--scene reference|cover] [--realm] [--width W]
-//           [--seed S] [--gpus N] [--out PATH] [--png PATH] [--json]
+//           [--seed S] [--gpus N] [--out PATH] [--png PATH] [--no-png] [--json]
 //           [--host-quantize]
 // Defaults follow the reference: spp 100, depth 50, width 400, 16:9.
 // --json: one more line, a JSON object of where this one-frame process's time
@@ -37,7 +39,7 @@ int main(int argc, char** argv) {
   int spp = 100, depth = 50, width = 400, gpus = 0, grid = 11;
   unsigned long long seed = 1;
   std::string scene = "reference", out, png;
-  bool realm = false, json = false, host_quantize = false;
+  bool realm = false, json = false, host_quantize = false, no_png = false;
   int pos = 0;
   const auto t_start = std::chrono::steady_clock::now();
   auto ms_since = [](std::chrono::steady_clock::time_point t) {
@@ -88,11 +90,19 @@ int main(int argc, char** argv) {
     else if (a == "--png") png = val();
     else if (a == "--realm") realm = true;
     else if (a == "--json") json = true;
+    else if (a == "--no-png") no_png = true;
     else if (a == "--host-quantize") host_quantize = true;
     else if (pos == 0) spp = std::atoi(argv[i]), ++pos;   // (:96)
     else if (pos == 1) depth = std::atoi(argv[i]), ++pos; // (:97)
   }
   if (out.empty()) out = realm ? "scene-realm.ppm" : "scene.ppm";
+  if (png.empty() && !no_png) {   // scene.ppm -> scene.png (raytracing.clj:176)
+    png = out;
+    const size_t dot = png.rfind(".ppm");
+    if (dot != std::string::npos && dot + 4 == png.size()) png.resize(dot);
+    png += ".png";
+  }
+  if (no_png) png.clear();
   if (!realm) std::printf("config: {:samples-per-px %d, :max-depth %d}\n", spp, depth);  // (:98)
   // -main: (int (/ image-width 16/9)) in exact ratios (:105-107); realm: a
   // double division by Ratio.doubleValue(16/9) = 1.777777777777778
@@ -160,12 +170,19 @@ int main(int argc, char** argv) {
     render_ms = ms_since(t0);
   }
   const auto t_w = std::chrono::steady_clock::now();
-  if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK ||
-      (!png.empty() && rt_write_png(png.c_str(), q.data(), width, height) != RT_OK)) {
+  if (rt_write_ppm(out.c_str(), q.data(), width, height) != RT_OK) {
     std::fprintf(stderr, "%s\n", rt_last_error());
     return 1;
   }
   const double write_ms = ms_since(t_w);
+  // (ppm->png "scene.ppm" "scene.png"): the reference reads the PPM it wrote
+  // back and encodes it (ppm2png.clj:35-87); so does this, inside the timing
+  const auto t_p = std::chrono::steady_clock::now();
+  if (!png.empty() && rt_ppm_to_png(out.c_str(), png.c_str()) != RT_OK) {
+    std::fprintf(stderr, "%s\n", rt_last_error());
+    return 1;
+  }
+  const double png_ms = png.empty() ? 0.0 : ms_since(t_p);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::printf("\"Elapsed time: %.3f msecs\"\n", ms);  // (time ...) (:99)
   std::printf("bodies %d, devices %d, kernel %.3f ms, %.1f Msamples/s, %.3f segments/sample\n", n,
@@ -176,12 +193,12 @@ int main(int argc, char** argv) {
         "{\"devices_visible\": %d, \"scene_ms\": %.3f, \"device_count_ms\": %.3f, \"prepare_ms\": {\"context\": %.3f, "
         "\"code_object\": %.3f, \"queue\": %.3f, \"pageable_staging\": %.3f}, \"prepare_wait_ms\": %.3f, "
         "\"render_ms\": %.3f, \"quantize\": \"%s\", "
-        "\"quantize_ms\": %.3f, \"write_ms\": %.3f, \"process_ms\": %.3f, \"rt_stats\": {\"total_ms\": %.3f, "
+        "\"quantize_ms\": %.3f, \"write_ms\": %.3f, \"png_ms\": %.3f, \"process_ms\": %.3f, \"rt_stats\": {\"total_ms\": %.3f, "
         "\"upload_ms\": %.3f, \"setup_ms\": %.3f, \"enqueue_ms\": %.3f, \"wait_ms\": %.3f, \"scatter_ms\": %.3f, "
         "\"other_ms\": %.3f, \"kernel_ms\": %.3f, \"d2h_ms\": %.3f, \"segments\": %llu, \"samples\": %llu, "
         "\"n_devices\": %d}}\n",
         ndev, scene_ms, device_count_ms, prep_ms[0], prep_ms[1], prep_ms[2], prep_ms[3], prep_wait_ms, render_ms,
-        host_quantize ? "host" : "device", quantize_ms, write_ms, ms_since(t_start), st.total_ms,
+        host_quantize ? "host" : "device", quantize_ms, write_ms, png_ms, ms_since(t_start), st.total_ms,
         st.upload_ms, st.setup_ms, st.enqueue_ms, st.wait_ms, st.scatter_ms, st.other_ms, st.kernel_ms, st.d2h_ms,
         static_cast<unsigned long long>(st.segments), static_cast<unsigned long long>(st.samples), st.n_devices);
   return 0;

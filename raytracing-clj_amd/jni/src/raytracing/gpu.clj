@@ -96,7 +96,8 @@
 
 (defn -main
   "`clojure -M:main [spp] [depth]` (raytracing.clj:95-177) on the GPU: the
-  same config line, (time ...) around render + PPM, scene.ppm."
+  same config line, (time ...) around render + PPM + PNG (scene.ppm, then
+  ppm->png to scene.png inside the timing, as raytracing.clj:176 does)."
   [& args]
   (let [spp (if (first args) (Integer/parseInt (first args)) 100)
         depth (if (second args) (Integer/parseInt (second args)) 50)
@@ -107,4 +108,5 @@
      (let [cam (camera width height {:vfov 20.0 :look-from [-2.0 2.0 1.0] :look-at [0.0 0.0 -1.0]
                                      :vup [0.0 1.0 0.0] :defocus-angle 10.0 :focus-dist 3.4})
            rgb (render-bytes hittables cam {:width width :height height :samples-per-px spp :max-depth depth})]
-       (write-ppm! "scene.ppm" rgb width height)))))
+       (write-ppm! "scene.ppm" rgb width height)
+       (ppm->png "scene.ppm" "scene.png")))))

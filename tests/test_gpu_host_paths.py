@@ -11,6 +11,7 @@ the same pixels.
 """
 from __future__ import annotations
 
+import json
 import os
 import subprocess
 from pathlib import Path
@@ -89,11 +90,19 @@ def test_rt_main_cover_scene(gpu_lib, tmp_path):
     C++ host at another width and seed."""
     from rtclj import raytracing as R
     from rtclj import scenes
-    _run(["4", "50", "--scene", "cover", "--width", "160", "--seed", "9", "--out", "c.ppm"], tmp_path)
+    from pngdec import decode
+    out = _run(["4", "50", "--scene", "cover", "--width", "160", "--seed", "9", "--out", "c.ppm", "--json"], tmp_path)
     img = R.read_ppm(tmp_path / "c.ppm")
     h = R.image_height(160)
     ref, _ = _mirror_q8(oracle.MODE_MIRROR32, scenes.cover(11), scenes.cover_camera(160, h), 160, h, 4, 50, seed=9)
     assert np.array_equal(img, ref)
+    # like -main's (ppm->png "scene.ppm" "scene.png") (raytracing.clj:176): the
+    # PPM is converted beside it by default, inside the timed part
+    assert np.array_equal(decode((tmp_path / "c.png").read_bytes())[0], img)
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert rec["png_ms"] > 0 and rec["process_ms"] >= rec["png_ms"]
+    _run(["1", "5", "--scene", "cover", "--width", "64", "--out", "n.ppm", "--no-png"], tmp_path)
+    assert (tmp_path / "n.ppm").exists() and not (tmp_path / "n.png").exists()
 
 
 def test_prepare_and_first_context_streams(gpu_lib):

@@ -26,9 +26,19 @@ def main():
     g = avg.get("GRBM_GUI_ACTIVE")
     if g:
         cyc = g / 8
-        if "SQ_ACTIVE_INST_VALU" in avg:
-            lines.append(f"  issue_busy   = SQ_ACTIVE_INST_VALU*4/1024 / (GRBM_GUI_ACTIVE/8) = "
-                         f"{avg['SQ_ACTIVE_INST_VALU'] * 4 / 1024 / cyc:.3f}")
+        if "SQ_ACTIVE_INST_VALU2" in avg:
+            busy = avg["SQ_ACTIVE_INST_VALU"] - avg["SQ_ACTIVE_INST_VALU2"]
+            lines.append(f"  valu_busy    = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) / (1024 SIMDs x cycles/4) = "
+                         f"{busy / (1024 * cyc / 4):.3f}")
+            lines.append(f"  dual_issue   = ACTIVE_INST_VALU2 / busy quad-cycles = {avg['SQ_ACTIVE_INST_VALU2'] / busy:.3f}")
+        if "SQ_INSTS_VALU" in avg:
+            lines.append(f"  valu_pipe_util = SQ_INSTS_VALU*2 / (1024 x cycles) = {avg['SQ_INSTS_VALU'] * 2 / 1024 / cyc:.3f}")
+        if "SQ_INSTS_SALU" in avg and "SQ_INSTS_VALU" in avg:
+            lines.append(f"  salu_per_valu = {avg['SQ_INSTS_SALU'] / avg['SQ_INSTS_VALU']:.3f}")
+        if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
+            wc = avg["SQ_WAVE_CYCLES"]
+            lines.append(f"  wait_dep {avg['SQ_WAIT_ANY'] / wc:.3f}  wait_issue {avg['SQ_WAIT_INST_ANY'] / wc:.3f}  "
+                         f"issuing {avg.get('SQ_ACTIVE_INST_ANY', 0) / wc:.3f} (of wave residency)")
         if "SQ_WAVE_CYCLES" in avg:
             lines.append(f"  waves/SIMD   = SQ_WAVE_CYCLES*4/1024 / (GRBM_GUI_ACTIVE/8) = "
                          f"{avg['SQ_WAVE_CYCLES'] * 4 / 1024 / cyc:.3f}")
