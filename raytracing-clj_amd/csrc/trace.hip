@@ -608,17 +608,16 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
 }
 
 // The compact variant (22) for a launch: the 4-body tree's node indices fit
-// a byte, and a pixel's u32 sum cannot overflow -- every sample's colour is
-// at most 1 per channel (albedos within [-1, 1]: the sky and the dielectric
-// give at most 1) and a pixel gets at most spp <= 255 samples, 255 * 2^24 <
-// 2^32.  The default selector runs it wherever it applies (and an explicit
-// 22 too); elsewhere the launch runs 16.  Seven workgroups per CU instead of
-// six, in 72 VGPRs without a spill: C1 5.90 -> 5.83 ms (profiles/r04/w7/,
-// DESIGN.md §8.1).
-// Its pixel table packs a pixel's image coordinates as x | y << 16: frames
-// up to 65536 pixels wide and high (wider or taller ones run 16).
+// a byte, and a pixel's u32 sum with its byte of wrap counts cannot overflow
+// -- every sample's colour is at most 1 per channel (albedos within [-1, 1]:
+// the sky and the dielectric give at most 1), so a channel wraps at most spp /
+// 256 < 256 times for spp < 65536 (none for spp <= 255, where the kernel adds
+// without counting).  Its pixel table packs no coordinates above 65535 (the
+// key table plus one image row per tile row).  The default selector runs it
+// wherever it applies (and an explicit 22 too); elsewhere the launch runs 16.
+// Seven workgroups per CU instead of six, in 72 VGPRs without a spill.
 static bool compact_ok(const rt_dscene& ds, const rt_params& p) {
-  return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp <= 255 && ds.tree[1].depth + 2 <= kBvhStack &&
+  return ds.unit_albedo && ds.tree[1].n_nodes <= 256 && p.spp < 65536 && ds.tree[1].depth + 2 <= kBvhStack &&
          p.width <= 65536 && p.height <= 65536;
 }
 static int launch_variant(const rt_dscene& ds, const rt_params& p) {

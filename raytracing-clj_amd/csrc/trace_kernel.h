@@ -604,6 +604,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // q / vw by multiply-high (exact: q < 64, vw <= 8)
   const int pool = (cnt > 0 && ka->max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
+  const uint32_t mag16_vw = vw > 0 ? (65536u + static_cast<uint32_t>(vw) - 1u) / static_cast<uint32_t>(vw) : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
   // the unit's LDS state.  The owner of a whole tile of more than 512
   // samples shares it: the tile's word with this launch's epoch, its lanes'
@@ -645,20 +646,33 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
   // image has no room for it: C4 keeps 5 workgroups per CU)
   constexpr bool kPixelTable = is_q(SCAN);
-  // (the compact variant: key and (x | y << 16) in 8 bytes)
-  using PxT = std::conditional_t<SCAN == SCAN_BVHQ7, uint2, float4>;
-  __shared__ PxT s_px[kPixelTable ? NPX : 1];
+  // (the compact variant: the keys alone, 4 bytes a pixel, and the image row
+  // of each of the tile's rows as a float; a pixel's column is q mod vw)
+  constexpr bool kCompactPx = SCAN == SCAN_BVHQ7;
+  __shared__ std::conditional_t<kCompactPx, uint32_t, float4> s_px[kPixelTable ? NPX : 1];
+  __shared__ float s_prow[kCompactPx ? TH : 1];
   if constexpr (kPixelTable) {
     const int t = static_cast<int>(threadIdx.x);
     if (t < npx) {
       const int qy = vw == 1 ? t : static_cast<int>(__umulhi(static_cast<uint32_t>(t), mag_vw));
       const int px = qx0 + (t - qy * vw);
       const int gy = image_row(qy0 + qy);
-      if constexpr (SCAN == SCAN_BVHQ7)
-        s_px[t] = make_uint2(pixel_key(px, gy), static_cast<unsigned>(px) | (static_cast<unsigned>(gy) << 16));
-      else
+      if constexpr (kCompactPx) {
+        s_px[t] = pixel_key(px, gy);
+        if (px == qx0) s_prow[qy] = static_cast<float>(gy);
+      } else {
         s_px[t] = make_float4(__uint_as_float(pixel_key(px, gy)), static_cast<float>(px), static_cast<float>(gy), 0.0f);
+      }
     }
+  }
+  // The compact variant's u32 pixel sums, when a pixel may get more than 255
+  // samples (spp > 255): a sum's wraps past 2^32 counted per channel in a
+  // byte of s_carry (a sample adds less than 2^32, so at most one wrap; with
+  // every colour <= 1 per channel a channel wraps at most spp / 256 < 256
+  // times for spp < 65536, compact_ok): its total is carry * 2^32 + sum.
+  __shared__ uint32_t s_carry[kCompactPx ? NPX * 3 / 4 : 1];
+  if constexpr (kCompactPx) {
+    if (threadIdx.x < NPX * 3 / 4) s_carry[threadIdx.x] = 0u;
   }
   __syncthreads();
   // the wave's batch [wb, we) of pool indices (wave-uniform; empty at first:
@@ -826,11 +840,12 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       q = j - k * npx;
       uint32_t pk;
       float fpx, fgy;
-      if constexpr (kPixelTable && SCAN == SCAN_BVHQ7) {
-        const uint2 pt = s_px[q];
-        pk = pt.x;
-        fpx = static_cast<float>(pt.y & 0xffffu);
-        fgy = static_cast<float>(pt.y >> 16);
+      if constexpr (kPixelTable && kCompactPx) {
+        pk = s_px[q];
+        // q / vw as (q * ceil(2^16 / vw)) >> 16: exact for q < 64, vw <= 8, vw = 1 included
+        const int qy = static_cast<int>(__umul24(static_cast<uint32_t>(q), mag16_vw) >> 16);
+        fpx = static_cast<float>(qx0 + (q - qy * vw));
+        fgy = s_prow[qy];
       } else if constexpr (kPixelTable) {   // the pixel's key and coordinates from the tile's table
         const float4 pt = s_px[q];
         pk = __float_as_uint(pt.x);
@@ -1440,9 +1455,24 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     if (done) {   // the sample's colour into its pixel's fixed-point sum (order-free)
       if constexpr (STATS) st_fl += 3;
       AccT* acc = &s_acc[q * 3];
-      __hip_atomic_fetch_add(acc + 0, static_cast<AccT>(fix24(cr)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(acc + 1, static_cast<AccT>(fix24(cg)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(acc + 2, static_cast<AccT>(fix24(cb)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (kCompactPx && sgpr(kargs_opaque()->spp) > 255) {
+        // the u32 sums with their wraps counted (s_carry above)
+        const uint32_t f0 = fix24(cr), f1 = fix24(cg), f2 = fix24(cb);
+        const uint32_t o0 = __hip_atomic_fetch_add(acc + 0, f0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t o1 = __hip_atomic_fetch_add(acc + 1, f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t o2 = __hip_atomic_fetch_add(acc + 2, f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool w0 = o0 + f0 < o0, w1 = o1 + f1 < o1, w2 = o2 + f2 < o2;
+        if (w0 | w1 | w2) {
+          const int c = q * 3;
+          if (w0) atomicAdd(&s_carry[c >> 2], 1u << (8 * (c & 3)));
+          if (w1) atomicAdd(&s_carry[(c + 1) >> 2], 1u << (8 * ((c + 1) & 3)));
+          if (w2) atomicAdd(&s_carry[(c + 2) >> 2], 1u << (8 * ((c + 2) & 3)));
+        }
+      } else {
+        __hip_atomic_fetch_add(acc + 0, static_cast<AccT>(fix24(cr)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(acc + 1, static_cast<AccT>(fix24(cg)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(acc + 2, static_cast<AccT>(fix24(cb)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
     // refill: the lanes whose paths ended take their next indices
     const uint64_t m = __ballot(done);
@@ -1551,19 +1581,28 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     // realm: pixel-scale = 1/spp, multiplied (realm/raytracing.clj:25, :276)
     ke->out[e] = ke->realm ? tot * (1.0f / inv) : tot / inv;
   };
+  // channel t's integer sum (the compact variant: its wraps added back)
+  auto total = [&](int tt) -> unsigned long long {
+    unsigned long long v = static_cast<unsigned long long>(s_acc[tt]);
+    if constexpr (kCompactPx) v += static_cast<unsigned long long>((s_carry[tt >> 2] >> (8 * (tt & 3))) & 0xffu) << 32;
+    return v;
+  };
   if (split) {   // one split's integer sums, added to the tile's (order-free); finalize_kernel converts them
-    if (t < npx * 3 && s_acc[t])
-      __hip_atomic_fetch_add(&ke->part[out_index(t)], static_cast<unsigned long long>(s_acc[t]), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    if (t < npx * 3) {
+      const unsigned long long v = total(t);
+      if (v) __hip_atomic_fetch_add(&ke->part[out_index(t)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   } else if (alone) {   // every sample of the tile was this workgroup's
-    if (t < npx * 3) write_mean(out_index(t), static_cast<unsigned long long>(s_acc[t]));
+    if (t < npx * 3) write_mean(out_index(t), total(t));
   } else {
     // a shared tile (owner or helper): the integer sums
     // meet in sum[tile] (atomics: any order, the same total); the workgroup
     // whose samples complete the pool converts them and re-zeroes the slots
     unsigned long long* gs = ke->sum + static_cast<size_t>(tile) * (NPX * 3);
-    if (t < npx * 3 && s_acc[t])
-      __hip_atomic_fetch_add(&gs[t], static_cast<unsigned long long>(s_acc[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < npx * 3) {
+      const unsigned long long v = total(t);
+      if (v) __hip_atomic_fetch_add(&gs[t], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
