@@ -380,6 +380,37 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
     u8_med = u8_runs[len(u8_runs) // 2]
     u8_equal = bool(np.array_equal(b8, R.write_color(out)))
 
+    # frames in flight through the product entry (rt_render_submit ..
+    # rt_render_wait): a frame loop keeping `nfl` frames submitted, each into
+    # its own framebuffer; frame k+1's shards start on the devices while
+    # frame k's rows come back
+    nfl = 2
+    bufs = [np.empty_like(out) for _ in range(nfl)]
+    for i in range(warm):
+        R.render_async(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags, out=bufs[i % nfl]).wait()
+    n_frames = max(4 * reps, 8)
+    pending = []
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        if len(pending) == nfl:
+            pending.pop(0).wait()
+        pending.append(R.render_async(scene, cam, W, H, spp, depth, seed=seed, n_devices=n_dev, flags=flags,
+                                      out=bufs[i % nfl]))
+    last = {}
+    for f in pending[:-1]:
+        f.wait()
+    pending[-1].wait(stats=last)
+    async_s = time.perf_counter() - t0
+    async_equal = all(bool(np.array_equal(b, out)) for b in bufs)
+    inflight = {"entry": "rt_render_submit .. rt_render_wait (include/rt.h)", "frames_in_flight": nfl,
+                "frames": n_frames, "seconds": async_s, "ms_per_frame": async_s / n_frames * 1e3,
+                "value": W * H * spp * n_frames / async_s / 1e6, "unit": "Mray-samples/s",
+                "kernel_ms_max_last": last.get("kernel_ms"), "equals_rt_render": async_equal,
+                "note": "a frame loop through the product entry: each frame submitted while the one before is still "
+                        "on the devices (its shards' launches split for two rounds of workgroups, "
+                        "RT_FLAG_STREAMED), waited on in order, every frame into one of two framebuffers; the "
+                        "host wall clock over all frames"}
+
     def parts(r):
         return {k: r[k] for k in PARTS}
 
@@ -401,7 +432,7 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
                       "total_ms": u8_med["total_ms"], "kernel_ms_max": u8_med["kernel_ms"],
                       "d2h_ms": u8_med["d2h_ms"], "equals_rt_quantize_of_rt_render": u8_equal,
                       "note": "d2h_ms includes the quantise kernel"},
-            "repeats": reps, "warm_calls": warm}, out
+            "frames_in_flight": inflight, "repeats": reps, "warm_calls": warm}, out
 
 
 def first_process(wl, spp, depth, seed, n_dev):

@@ -239,6 +239,26 @@ int rt_render(const rt_scene* s, const rt_camera* c, const rt_params* p,
 int rt_render_u8(const rt_scene* s, const rt_camera* c, const rt_params* p,
                  uint8_t* out_rgb8, size_t out_len, rt_stats* stats);
 
+/* ---- frames in flight: a host drawing a sequence of frames ---------------
+ * rt_render_submit starts the frame rt_render would render -- the same
+ * shards, scene cache, devices and bits -- and returns without waiting for
+ * the devices; rt_render_wait blocks until the frame's rows are in out_rgb
+ * (which the caller leaves alone until then), fills stats as rt_render does
+ * and frees the frame.  Frames submitted before earlier ones are waited on
+ * run concurrently: each frame in flight holds its own render context
+ * (stream, device buffers) per device, and its launches split their tiles'
+ * samples for two rounds of workgroups (RT_FLAG_STREAMED), so the next
+ * frame's workgroups fill this one's tail.  Every submitted frame must be
+ * waited on exactly once, from any thread.  (raytracing.clj:157-171's
+ * executor hands its futures back the same way: submit, then .get in order.)
+ * The _u8 form delivers rt_render_u8's bytes. */
+typedef struct rt_frame rt_frame;
+int rt_render_submit(const rt_scene* s, const rt_camera* c, const rt_params* p, float* out_rgb,
+                     size_t out_len, rt_frame** frame);
+int rt_render_submit_u8(const rt_scene* s, const rt_camera* c, const rt_params* p, uint8_t* out_rgb8,
+                        size_t out_len, rt_frame** frame);
+int rt_render_wait(rt_frame* frame, rt_stats* stats);
+
 /* Drop rt_render's cached device scenes and render contexts (streams,
  * buffers; those not in use by a concurrent call).  Returns the number of
  * scenes dropped. */

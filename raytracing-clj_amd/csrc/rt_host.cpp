@@ -499,40 +499,81 @@ struct Shard {
   double upload_ms = 0.0, setup_ms = 0.0, enqueue_ms = 0.0, wait_ms = 0.0, scatter_ms = 0.0, wall_ms = 0.0;
   double gather_ms = 0.0;   // d2h_ms (+ scatter_ms, 0: no host scatter)
   bool cached = false;
+  // between start_shard and finish_shard: the share's context (its stream,
+  // device buffers) and scene, held by the frame
+  std::unique_ptr<Ctx> cx;
+  std::shared_ptr<rt_dscene> ds;
+  Clock::time_point t0;
+  bool gathered = false;   // the D2H is already enqueued behind the launch
 };
 
-// one device's share: scene (cached), launch, D2H of its compacted row
-// tiles straight into their rows of out_rgb (disjoint rows: the shards copy
-// in parallel, each as soon as its own device is done).  u8: out_rgb is
-// bytes, quantised on the device after the launch (rt_render_u8)
-void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, bool u8, int rows_total,
-               int ntiles, int nshards, int shard_idx) {
-  auto fail = [&](int code) {
-    sh->status = code;
-    sh->err = rt_last_error();
-  };
+// The shard's compacted row tiles, D2H straight into their rows of out_rgb
+// (measured on MI355X for a C1 frame: 0.46-0.52 ms, against 0.53-0.56 ms
+// into pinned staging plus 0.34 ms of host copy, tools/d2h_bench.cpp).
+// Several shards: tile k of the shard -> image tile shard_idx + k * nshards,
+// through one strided copy, the image's last tile, if it is short, a second.
+// Then the counters.  Enqueued on the context's stream.
+hipError_t enqueue_gather(Shard* sh, void* out_rgb, bool u8, int rows_total, int ntiles, int nshards, int shard_idx) {
+  Ctx* cx = sh->cx.get();
+  const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
+  const void* src = u8 ? static_cast<const void*>(cx->d_u8) : static_cast<const void*>(cx->d_out);
+  const size_t es = u8 ? 1 : sizeof(float);
+  hipError_t e = hipSuccess;
+  if (nfl) {
+    if (nshards == 1) {
+      e = hipMemcpyAsync(out_rgb, src, nfl * es, hipMemcpyDeviceToHost, cx->stream);
+    } else {
+      const int T = sh->p.row_tile;
+      const size_t rowb = static_cast<size_t>(sh->p.width) * 3 * es;
+      const int ntile = (ntiles - shard_idx + nshards - 1) / nshards;   // this shard's tiles
+      const int t_last = shard_idx + (ntile - 1) * nshards;
+      const bool short_last = t_last == ntiles - 1 && rows_total % T != 0;
+      const int nfull = ntile - (short_last ? 1 : 0);
+      if (nfull > 0)
+        e = hipMemcpy2DAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(shard_idx) * T * rowb,
+                             static_cast<size_t>(nshards) * T * rowb, src, T * rowb, T * rowb, nfull,
+                             hipMemcpyDeviceToHost, cx->stream);
+      if (e == hipSuccess && short_last)
+        e = hipMemcpyAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(t_last) * T * rowb,
+                           static_cast<const char*>(src) + static_cast<size_t>(nfull) * T * rowb,
+                           static_cast<size_t>(rows_total - t_last * T) * rowb, hipMemcpyDeviceToHost, cx->stream);
+    }
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(cx->h_cnt, cx->d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, cx->stream);
+  if (e == hipSuccess) e = hipEventRecord(cx->e2, cx->stream);
+  return e;
+}
+
+// One device's share, first half: scene (cached), render context, launch
+// (and the device quantiser for u8).  gather_now: the D2H into out_rgb is
+// enqueued right behind the launch (rt_render); otherwise finish_shard does
+// it once the device is done (rt_render_submit: a copy into pageable memory
+// would hold the host until the kernel ends).  On failure sh->status is set
+// and the context released.
+void start_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, bool u8, bool gather_now,
+                 int rows_total, int ntiles, int nshards, int shard_idx) {
   auto hip_fail = [&](hipError_t e, const char* what) {
     sh->status = RT_E_HIP;
     sh->err = std::string(what) + ": " + hipGetErrorString(e);
   };
-  const auto t0 = Clock::now();
-  std::shared_ptr<rt_dscene> ds;
+  sh->t0 = Clock::now();
   int rc = RT_OK;
   // the scene: from the cache, or (a miss: upload and BVH builds, ~1-3 ms)
   // on a helper thread while this one sets up the render context, the other
   // one-time cost of a first call (stream, events, buffers)
   std::thread upload;
   std::string upload_err;   // (the error slot is per thread)
-  if (!find_scene(sh->device, s, &ds)) {
+  if (!find_scene(sh->device, s, &sh->ds)) {
     upload = std::thread([&] {
-      rc = get_scene(sh->device, s, &ds, &sh->cached);
+      rc = get_scene(sh->device, s, &sh->ds, &sh->cached);
       if (rc != RT_OK) upload_err = rt_last_error();
     });
   } else {
     sh->cached = true;
   }
   const auto t_setup = Clock::now();
-  std::unique_ptr<Ctx> cx = take_ctx(sh->device);
+  sh->cx = take_ctx(sh->device);
+  Ctx* cx = sh->cx.get();
   const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
   hipError_t e = hipSetDevice(sh->device);
   if (e == hipSuccess && !cx->stream && !cx->null_stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
@@ -561,7 +602,8 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, 
   if (upload.joinable()) upload.join();
   sh->upload_ms = ms_since(t_up);
   if (rc != RT_OK) {
-    if (e == hipSuccess) give_ctx(std::move(cx));
+    if (e == hipSuccess) give_ctx(std::move(sh->cx));
+    sh->cx.reset();
     sh->status = rc;
     sh->err = upload_err;
     return;
@@ -571,66 +613,60 @@ void run_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb, 
   if (e == hipSuccess) e = hipEventRecord(cx->e0, cx->stream);
   if (e != hipSuccess) {
     hip_fail(e, "rt_render setup");
-  } else {
-    cx->launched(ds.get());   // (before the launch: it may have made the stream's entry and then failed)
-    rc = rt_launch(ds.get(), c, &sh->p, cx->d_out, cx->d_cnt, cx->stream);
-    if (rc != RT_OK) {
-      fail(rc);
-    } else {
-      e = hipEventRecord(cx->e1, cx->stream);
-      // (u8: the quantiser's few microseconds fall in d2h_ms)
-      if (e == hipSuccess && u8 && nfl) e = static_cast<hipError_t>(quantize_launch(cx->d_out, cx->d_u8, nfl, cx->stream));
-      const void* src = u8 ? static_cast<const void*>(cx->d_u8) : static_cast<const void*>(cx->d_out);
-      const size_t es = u8 ? 1 : sizeof(float);
-      // straight into the caller's buffer (measured on MI355X for a C1
-      // frame: 0.46-0.52 ms, against 0.53-0.56 ms into pinned staging plus
-      // 0.34 ms of host copy, tools/d2h_bench.cpp).  Several shards: the
-      // shard's compacted row tiles land in their image rows through one
-      // strided copy (tile k of the shard -> image tile shard_idx + k *
-      // nshards), the image's last tile, if it is short, through a second
-      if (e == hipSuccess && nfl) {
-        if (nshards == 1) {
-          e = hipMemcpyAsync(out_rgb, src, nfl * es, hipMemcpyDeviceToHost, cx->stream);
-        } else {
-          const int T = sh->p.row_tile;
-          const size_t rowb = static_cast<size_t>(sh->p.width) * 3 * es;
-          const int ntile = (ntiles - shard_idx + nshards - 1) / nshards;   // this shard's tiles
-          const int t_last = shard_idx + (ntile - 1) * nshards;
-          const bool short_last = t_last == ntiles - 1 && rows_total % T != 0;
-          const int nfull = ntile - (short_last ? 1 : 0);
-          if (nfull > 0)
-            e = hipMemcpy2DAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(shard_idx) * T * rowb,
-                                 static_cast<size_t>(nshards) * T * rowb, src, T * rowb, T * rowb, nfull,
-                                 hipMemcpyDeviceToHost, cx->stream);
-          if (e == hipSuccess && short_last)
-            e = hipMemcpyAsync(reinterpret_cast<char*>(out_rgb) + static_cast<size_t>(t_last) * T * rowb,
-                               static_cast<const char*>(src) + static_cast<size_t>(nfull) * T * rowb,
-                               static_cast<size_t>(rows_total - t_last * T) * rowb, hipMemcpyDeviceToHost, cx->stream);
-        }
-      }
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(cx->h_cnt, cx->d_cnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, cx->stream);
-      if (e == hipSuccess) e = hipEventRecord(cx->e2, cx->stream);
-      sh->enqueue_ms = ms_since(t_enq);
-      const auto t_wait = Clock::now();
-      if (e == hipSuccess) e = hipStreamSynchronize(cx->stream);
-      sh->wait_ms = ms_since(t_wait);
-      float d2h = 0.0f;
-      if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, cx->e0, cx->e1);
-      if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->e1, cx->e2);
-      sh->d2h_ms = d2h;
-      if (e != hipSuccess) {
-        hip_fail(e, "rt_render trace/gather");
-      } else {
-        sh->counters[0] = cx->h_cnt[0];
-        sh->counters[1] = cx->h_cnt[1];
-        sh->scatter_ms = 0.0;   // (no host scatter: the copies place the rows)
-        sh->gather_ms = d2h;
-      }
-    }
+    return;
   }
-  sh->wall_ms = ms_since(t0);
-  if (sh->status == RT_OK) give_ctx(std::move(cx));
+  cx->launched(sh->ds.get());   // (before the launch: it may have made the stream's entry and then failed)
+  rc = rt_launch(sh->ds.get(), c, &sh->p, cx->d_out, cx->d_cnt, cx->stream);
+  if (rc != RT_OK) {
+    sh->status = rc;
+    sh->err = rt_last_error();
+    return;
+  }
+  e = hipEventRecord(cx->e1, cx->stream);
+  // (u8: the quantiser's few microseconds fall in d2h_ms)
+  if (e == hipSuccess && u8 && nfl) e = static_cast<hipError_t>(quantize_launch(cx->d_out, cx->d_u8, nfl, cx->stream));
+  if (e == hipSuccess && gather_now) {
+    e = enqueue_gather(sh, out_rgb, u8, rows_total, ntiles, nshards, shard_idx);
+    sh->gathered = true;
+  }
+  sh->enqueue_ms = ms_since(t_enq);
+  if (e != hipSuccess) hip_fail(e, "rt_render launch/gather");
+}
+
+// Second half: wait for the device (and the D2H, enqueued here if it was
+// not), the share's counters and event times; the context goes back to the
+// device's pool (a failed one is dropped: its stream may hold a fault).
+void finish_shard(Shard* sh, void* out_rgb, bool u8, int rows_total, int ntiles, int nshards, int shard_idx) {
+  Ctx* cx = sh->cx.get();
+  if (sh->status == RT_OK && cx) {
+    const auto t_wait = Clock::now();
+    hipError_t e = hipSetDevice(sh->device);
+    if (e == hipSuccess && !sh->gathered) e = hipStreamSynchronize(cx->stream);
+    if (e == hipSuccess && !sh->gathered) e = enqueue_gather(sh, out_rgb, u8, rows_total, ntiles, nshards, shard_idx);
+    if (e == hipSuccess) e = hipStreamSynchronize(cx->stream);
+    sh->wait_ms = ms_since(t_wait);
+    float d2h = 0.0f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, cx->e0, cx->e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->e1, cx->e2);
+    sh->d2h_ms = d2h;
+    if (e != hipSuccess) {
+      sh->status = RT_E_HIP;
+      sh->err = std::string("rt_render trace/gather: ") + hipGetErrorString(e);
+    } else {
+      sh->counters[0] = cx->h_cnt[0];
+      sh->counters[1] = cx->h_cnt[1];
+      sh->scatter_ms = 0.0;   // (no host scatter: the copies place the rows)
+      sh->gather_ms = d2h;
+    }
+  } else if (cx) {
+    // a failed start: wait for whatever it enqueued before the context is dropped
+    (void)hipSetDevice(sh->device);
+    (void)hipStreamSynchronize(cx->stream);
+  }
+  sh->wall_ms = ms_since(sh->t0);
+  if (sh->status == RT_OK && sh->cx) give_ctx(std::move(sh->cx));
+  sh->cx.reset();
+  sh->ds.reset();
 }
 
 }  // namespace
@@ -655,41 +691,47 @@ extern "C" int rt_cache_clear(void) {
   return dropped;
 }
 
+// A frame in flight (rt_render, or rt_render_submit .. rt_render_wait): its
+// shards, each holding its device's render context until it finishes.
+struct rt_frame {
+  std::vector<Shard> shards;
+  void* out = nullptr;
+  bool u8 = false;
+  int rows = 0, ntiles = 0;
+  Clock::time_point t0;
+};
+
 namespace {
-// rt_render and rt_render_u8: out_rgb holds floats or (u8) bytes
-int render(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_rgb, bool u8, size_t out_len,
-           rt_stats* stats) {
-  clear_error();
-  const auto t0 = Clock::now();
-  if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, "rt_render: NULL argument");
+// The shards of a frame (argument checks as rt_render documents them).
+int plan_frame(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_rgb, bool u8, size_t out_len,
+               const char* who, rt_frame* f) {
+  const std::string w(who);
+  if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, w + ": NULL argument");
   const bool on_dev0 = (p->flags & RT_FLAG_SHARDS_ON_DEVICE0) != 0;
   if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP || p->n_devices < 0 ||
       (p->flags & ~(RT_FLAG_SHARDS_ON_DEVICE0 | RT_FLAG_REALM)) != 0 || (on_dev0 && p->n_devices == 0))
-    return set_error(RT_E_ARG, "rt_render: bad width/height/spp/flags/n_devices");
+    return set_error(RT_E_ARG, w + ": bad width/height/spp/flags/n_devices");
   if (p->tile_step != 0 || p->tile_first != 0)
-    return set_error(RT_E_ARG, "rt_render: tile_first/tile_step are per-shard (rt_launch) fields");
+    return set_error(RT_E_ARG, w + ": tile_first/tile_step are per-shard (rt_launch) fields");
   if (s->n < 0 || (s->n > 0 && (!s->sphere || !s->mat_kind || !s->mat)))
-    return set_error(RT_E_ARG, "rt_render: bad scene arrays");
+    return set_error(RT_E_ARG, w + ": bad scene arrays");
   const int rows = rows_out(*p);
-  if (rows < 0) return set_error(RT_E_ARG, "rt_render: bad row range");
+  if (rows < 0) return set_error(RT_E_ARG, w + ": bad row range");
   const size_t need = static_cast<size_t>(rows) * p->width * 3;
   if (out_len < need)
-    return set_error(RT_E_ARG, "rt_render: out_len " + std::to_string(out_len) + " < " + std::to_string(need));
+    return set_error(RT_E_ARG, w + ": out_len " + std::to_string(out_len) + " < " + std::to_string(need));
   const int ndev_vis = rt_device_count();
-  if (ndev_vis <= 0) return set_error(RT_E_NODEV, "rt_render: no GPU visible");
+  if (ndev_vis <= 0) return set_error(RT_E_NODEV, w + ": no GPU visible");
   int ndev = p->n_devices == 0 ? ndev_vis : p->n_devices;
   if (ndev > ndev_vis && !on_dev0)
-    return set_error(RT_E_NODEV, "rt_render: n_devices " + std::to_string(ndev) + " > visible " +
-                                     std::to_string(ndev_vis));
-  if (ndev_vis > static_cast<int>(g_cache->size()))
-    return set_error(RT_E_NODEV, "rt_render: more than 64 devices");
+    return set_error(RT_E_NODEV, w + ": n_devices " + std::to_string(ndev) + " > visible " + std::to_string(ndev_vis));
+  if (ndev_vis > static_cast<int>(g_cache->size())) return set_error(RT_E_NODEV, w + ": more than 64 devices");
   const int T = p->row_tile > 0 ? p->row_tile : 8;
   const int ntiles = (rows + T - 1) / T;
   ndev = std::max(1, std::min(ndev, std::max(ntiles, 1)));
-
-  std::vector<Shard> shards(ndev);
+  f->shards = std::vector<Shard>(ndev);
   for (int d = 0; d < ndev; ++d) {
-    Shard& sh = shards[d];
+    Shard& sh = f->shards[d];
     sh.device = on_dev0 ? 0 : d;
     sh.p = *p;
     sh.p.flags = p->flags & RT_FLAG_REALM;   // semantics travel; the fan-out flag is rt_render's
@@ -700,21 +742,36 @@ int render(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_
     }
     sh.rows = rows_out(sh.p);
   }
-  if (ndev == 1) {
-    run_shard(s, c, &shards[0], out_rgb, u8, rows, ntiles, 1, 0);
-  } else {
-    std::vector<std::function<void()>> tasks;
-    for (int d = 0; d < ndev; ++d)
-      tasks.emplace_back([=, &shards] { run_shard(s, c, &shards[d], out_rgb, u8, rows, ntiles, ndev, d); });
-    g_pool->run(tasks);
+  f->out = out_rgb;
+  f->u8 = u8;
+  f->rows = rows;
+  f->ntiles = ntiles;
+  return RT_OK;
+}
+
+// run fn(d) for every shard: the first on this thread, the others on the pool
+template <class F>
+void for_shards(rt_frame* f, F fn) {
+  const int n = static_cast<int>(f->shards.size());
+  if (n == 1) {
+    fn(0);
+    return;
   }
+  std::vector<std::function<void()>> tasks;
+  for (int d = 0; d < n; ++d) tasks.emplace_back([&fn, d] { fn(d); });
+  g_pool->run(tasks);
+}
+
+// the frame's statistics and status once every shard has finished
+int frame_result(rt_frame* f, rt_stats* stats) {
+  const int ndev = static_cast<int>(f->shards.size());
   double kms = 0, ksum = 0, ums = 0, gms = 0, d2h = 0;
   uint64_t segs = 0, smp = 0;
   int cached = 0, slowest = 0;
   for (int d = 0; d < ndev; ++d) {
-    Shard& sh = shards[d];
+    Shard& sh = f->shards[d];
     if (sh.status != RT_OK) return set_error(sh.status, "device " + std::to_string(d) + ": " + sh.err);
-    if (sh.wall_ms > shards[slowest].wall_ms) slowest = d;
+    if (sh.wall_ms > f->shards[slowest].wall_ms) slowest = d;
     d2h = std::max(d2h, static_cast<double>(sh.d2h_ms));
     kms = std::max(kms, static_cast<double>(sh.ms));
     ksum += sh.ms;
@@ -733,16 +790,33 @@ int render(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_
     stats->gather_ms = gms;
     stats->scene_cached = cached;
     stats->n_devices = ndev;
-    const Shard& sl = shards[slowest];
+    const Shard& sl = f->shards[slowest];
     stats->setup_ms = sl.setup_ms;
     stats->enqueue_ms = sl.enqueue_ms;
     stats->wait_ms = sl.wait_ms;
     stats->scatter_ms = sl.scatter_ms;
     stats->d2h_ms = d2h;
-    stats->total_ms = ms_since(t0);
+    stats->total_ms = ms_since(f->t0);
     stats->other_ms = stats->total_ms - (sl.upload_ms + sl.setup_ms + sl.enqueue_ms + sl.wait_ms + sl.scatter_ms);
   }
   return RT_OK;
+}
+
+// rt_render and rt_render_u8: out_rgb holds floats or (u8) bytes; each
+// device's share starts, gathers and finishes on its own host worker
+int render(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_rgb, bool u8, size_t out_len,
+           rt_stats* stats) {
+  clear_error();
+  rt_frame f;
+  f.t0 = Clock::now();
+  const int rc = plan_frame(s, c, p, out_rgb, u8, out_len, "rt_render", &f);
+  if (rc != RT_OK) return rc;
+  const int n = static_cast<int>(f.shards.size());
+  for_shards(&f, [&](int d) {
+    start_shard(s, c, &f.shards[d], out_rgb, u8, true, f.rows, f.ntiles, n, d);
+    finish_shard(&f.shards[d], out_rgb, u8, f.rows, f.ntiles, n, d);
+  });
+  return frame_result(&f, stats);
 }
 }  // namespace
 
@@ -754,6 +828,53 @@ extern "C" int rt_render(const rt_scene* s, const rt_camera* c, const rt_params*
 extern "C" int rt_render_u8(const rt_scene* s, const rt_camera* c, const rt_params* p, uint8_t* out_rgb8,
                             size_t out_len, rt_stats* stats) {
   return render(s, c, p, out_rgb8, true, out_len, stats);
+}
+
+namespace {
+int submit(const rt_scene* s, const rt_camera* c, const rt_params* p, void* out_rgb, bool u8, size_t out_len,
+           rt_frame** frame) {
+  clear_error();
+  if (!frame) return set_error(RT_E_ARG, "rt_render_submit: NULL frame");
+  *frame = nullptr;
+  auto f = std::make_unique<rt_frame>();
+  f->t0 = Clock::now();
+  const int rc = plan_frame(s, c, p, out_rgb, u8, out_len, "rt_render_submit", f.get());
+  if (rc != RT_OK) return rc;
+  const int n = static_cast<int>(f->shards.size());
+  // frames in flight: two rounds of split units per launch (RT_FLAG_STREAMED)
+  for (Shard& sh : f->shards) sh.p.flags |= RT_FLAG_STREAMED;
+  rt_frame* fp = f.get();
+  for_shards(fp, [&](int d) { start_shard(s, c, &fp->shards[d], out_rgb, u8, false, fp->rows, fp->ntiles, n, d); });
+  for (int d = 0; d < n; ++d)
+    if (fp->shards[d].status != RT_OK) {   // undo: wait for what did start, drop the frame
+      const std::string err = "device " + std::to_string(d) + ": " + fp->shards[d].err;
+      const int code = fp->shards[d].status;
+      for_shards(fp, [&](int k) { finish_shard(&fp->shards[k], out_rgb, u8, fp->rows, fp->ntiles, n, k); });
+      return set_error(code, err);
+    }
+  *frame = f.release();
+  return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_render_submit(const rt_scene* s, const rt_camera* c, const rt_params* p, float* out_rgb,
+                                size_t out_len, rt_frame** frame) {
+  return submit(s, c, p, out_rgb, false, out_len, frame);
+}
+
+extern "C" int rt_render_submit_u8(const rt_scene* s, const rt_camera* c, const rt_params* p, uint8_t* out_rgb8,
+                                   size_t out_len, rt_frame** frame) {
+  return submit(s, c, p, out_rgb8, true, out_len, frame);
+}
+
+extern "C" int rt_render_wait(rt_frame* frame, rt_stats* stats) {
+  clear_error();
+  if (!frame) return set_error(RT_E_ARG, "rt_render_wait: NULL frame");
+  std::unique_ptr<rt_frame> f(frame);
+  const int n = static_cast<int>(f->shards.size());
+  rt_frame* fp = f.get();
+  for_shards(fp, [&](int d) { finish_shard(&fp->shards[d], fp->out, fp->u8, fp->rows, fp->ntiles, n, d); });
+  return frame_result(fp, stats);
 }
 
 extern "C" int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_stream) {

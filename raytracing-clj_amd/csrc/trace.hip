@@ -210,7 +210,8 @@ static const Variant& variant_table(int v) {
   static const Variant v5{RT_K(SRC_SCALAR, SCAN_GROUP4, false), false, false, SCAN_GROUP4};
   static const Variant v12{RT_K(SRC_SCALAR, SCAN_BVH, false), false, false, SCAN_BVH};
   static const Variant v16{RT_K(SRC_LDS, SCAN_BVHQ, false), true, false, SCAN_BVHQ};
-  static const Variant v18{RT_K(SRC_LDS, SCAN_BVHO, false), true, false, SCAN_BVHO};
+  // (8-wave workgroups: one tree image for twice the waves)
+  static const Variant v18{RT_KW(SRC_LDS, SCAN_BVHO, false, 8), true, false, SCAN_BVHO, 512};
   static const Variant v22{RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7};
   switch (v) {
     case 0: return placeholder;
@@ -563,10 +564,13 @@ extern "C" int rt_scene_free(rt_dscene* d) {
 // traversal stack bytes: u8 entries for the 8-body-leaf tree (tree[2], at
 // most 256 nodes when its variant runs), u16 otherwise
 static int stack_entries(const DTree& t, int tree) { return tree == 0 ? t.depth + 2 : std::max(t.depth, 1); }
-static size_t stack_of(const DTree& t, int tree) {
-  return static_cast<size_t>(stack_entries(t, tree)) * 256 * (tree == 2 ? 1 : 2);
+// (threads: the workgroup's lanes, a stack row each)
+static size_t stack_of(const DTree& t, int tree, int threads = 256) {
+  return static_cast<size_t>(stack_entries(t, tree)) * threads * (tree == 2 ? 1 : 2);
 }
-static size_t lds_of(const DTree& t, int tree) { return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree); }
+static size_t lds_of(const DTree& t, int tree, int threads = 256) {
+  return static_cast<size_t>(t.blob_f4) * 16 + stack_of(t, tree, threads);
+}
 // variant 22 (the compact image): u8 node indices, depth rows (the dead
 // far-child write goes one above the top, as in 16)
 static int stack_entries_compact(const DTree& t) { return std::max(t.depth, 1); }
@@ -636,7 +640,7 @@ static size_t launch_lds(const rt_dscene& ds, int vsel) {
   if (vsel == 22) return lds_of_compact(ds.tree[1]);
   if (vsel >= 11) {
     const DTree& tr = ds.tree[variant_tree(vsel)];
-    return v.lds ? lds_of(tr, variant_tree(vsel)) : stack_of(tr, variant_tree(vsel));
+    return v.lds ? lds_of(tr, variant_tree(vsel), v.threads) : stack_of(tr, variant_tree(vsel), v.threads);
   }
   return v.lds ? static_cast<size_t>(ds.n_pad) * sizeof(float4) : 0;
 }

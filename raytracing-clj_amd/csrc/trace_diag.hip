@@ -592,7 +592,7 @@ const Variant* diag_variant(int v) {
       {nullptr, false, false, 0},                                          // 16 (product)
       {RT_K(SRC_LDS, SCAN_BVHQ, true), true, true, SCAN_BVHQ},             // 17
       {nullptr, false, false, 0},                                          // 18 (product)
-      {RT_K(SRC_LDS, SCAN_BVHO, true), true, true, SCAN_BVHO},             // 19
+      {RT_KW(SRC_LDS, SCAN_BVHO, true, 8), true, true, SCAN_BVHO, 512},    // 19
       // direction-coherent waves (A/B, measured slower: profiles/r04/sorted_waves/):
       // octant-sorted, and lock-step packing only
       {reinterpret_cast<const void*>(&sorted_kernel<true>), true, false, SCAN_BVHS, kSortThreads},    // 20

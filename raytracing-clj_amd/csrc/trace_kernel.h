@@ -372,7 +372,12 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_
 // (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
 // waves; with it, a few of them spill to scratch outside the hot loop.
 constexpr int min_waves(int scan, bool stats) {
-  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 5 : 1;
+  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 6 : 1;
+}
+// __launch_bounds__'s minimum workgroups per CU for that many waves per SIMD
+// with NW-wave workgroups (4 SIMDs a CU)
+constexpr int min_blocks(int scan, bool stats, int nw) {
+  return (min_waves(scan, stats) * 4 + nw - 1) / nw;
 }
 
 // The diagnostic scans (SCAN_SIMPLE, SCAN_PK4: the linear scans of the A/B
@@ -382,8 +387,12 @@ template <int SRC, int SCAN, class F>
 __device__ void diag_scan(const struct KArgs& a, const float4* s_geo, float ox, float oy, float oz, float ux,
                           float uy, float uz, F&& consider);
 
-template <int SRC, int SCAN, bool STATS = false>
-__global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(const KArgs a) {
+// NW waves per workgroup (4; 8 for the 8-body-leaf walk, whose large LDS
+// image one workgroup of 8 waves shares: 3 workgroups = 6 waves per SIMD on
+// C4's 1000-body tree, where 4-wave workgroups fit 5 per CU = 5 waves)
+template <int SRC, int SCAN, bool STATS = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, min_blocks(SCAN, STATS, NW)) void trace_kernel(const KArgs a) {
+  constexpr int NT = 64 * NW;   // threads
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
   // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample
   // j / npx: the lanes ending paths together add into different pixels'
@@ -405,9 +414,9 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   __shared__ int s_last;
   // drain compaction: per wave the paths it posted and how many were taken;
   // the waves still in the hot loop
-  __shared__ int s_mb_post[4], s_mb_take[4], s_alive, s_mb_avail;
+  __shared__ int s_mb_post[NW], s_mb_take[NW], s_alive, s_mb_avail;
   // per wave: post when down to this many paths (0: posted once already; -1: off)
-  __shared__ int s_mb_lim[4];
+  __shared__ int s_mb_lim[NW];
   constexpr int TH = tile_rows(SCAN);   // tile rows
   constexpr int NPX = kTile * TH;       // pool pixels
   // the pool's pixel sums: u32 in the compact variant (the host runs it only
@@ -454,8 +463,8 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     const int M = ka->n_owner;
     const int w0 = static_cast<int>(mix32(static_cast<uint32_t>(unit)) % static_cast<uint32_t>(M));
     unsigned long long key = 0;
-    for (int i = 0; i < 2; ++i) {
-      int w = w0 + static_cast<int>(threadIdx.x) + 256 * i;
+    for (int i = 0; i < 512 / NT; ++i) {
+      int w = w0 + static_cast<int>(threadIdx.x) + NT * i;
       w = w >= M ? w - M : w;
       w = w >= M ? w % M : w;
       const int t = xload32(&ka->owner[w]);
@@ -475,11 +484,11 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       // join: one atomic counts the helper in and claims its lanes' first indices
       const int t = static_cast<int>(static_cast<unsigned>(best_key));
       const int P = tile_pool(ka, t);
-      const unsigned long long wd = __hip_atomic_fetch_add(&ka->word[t], (1ull << 32) + 256u, __ATOMIC_RELAXED,
+      const unsigned long long wd = __hip_atomic_fetch_add(&ka->word[t], (1ull << 32) + NT, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT);
       const int g = static_cast<int>(static_cast<unsigned>(wd));
       if (word_epoch(wd) == ka->epoch && g < P) {   // (another epoch: a spent word of an earlier launch)
-        const int got = min(P - g, 256);
+        const int got = min(P - g, NT);
         __hip_atomic_fetch_add(&ka->stealc[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(&ka->stealc[1], static_cast<unsigned long long>(got), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -507,7 +516,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       const int nodes_f4 = a.bvh_off_pairs >> 4;
       const int pairs_f4 = (a.bvh_off_pidx - a.bvh_off_pairs) >> 4;   // 2 per pair
       const int rec0 = nb0 + (nodes_f4 << 4);
-      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) {
+      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += NT) {
         float4 v = a.bvh_blob[i];
         int d = i;
         if (i < nodes_f4) {
@@ -533,10 +542,10 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
         s_geo[d] = v;
       }
     } else if constexpr (is_bvh_scan(SCAN)) {
-      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += 256) s_geo[i] = a.bvh_blob[i];
+      for (int i = threadIdx.x; i < a.bvh_blob_f4; i += NT) s_geo[i] = a.bvh_blob[i];
     } else {
       const float4* src = SCAN == SCAN_PK4 ? reinterpret_cast<const float4*>(a.geo2) : a.geo;
-      for (int i = threadIdx.x; i < a.n_pad; i += 256) s_geo[i] = src[i];
+      for (int i = threadIdx.x; i < a.n_pad; i += NT) s_geo[i] = src[i];
     }
   }
   uint32_t segs = 0;
@@ -624,18 +633,18 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   const int kc_batch_max = ka->batch_max > 0 ? ka->batch_max : min(1024, max(kShareBatch, (pool / 48) & ~63));
   if (threadIdx.x == 0) {
     if (own && shared_tile) {
-      __hip_atomic_exchange(&ka->word[tile], (static_cast<unsigned long long>(ka->epoch) << 48) | 256ull,
+      __hip_atomic_exchange(&ka->word[tile], (static_cast<unsigned long long>(ka->epoch) << 48) | static_cast<unsigned long long>(NT),
                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_exchange(&ka->owner[unit % ka->n_owner], tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_cnt = 256;
+      s_cnt = NT;
     }
     s_join = own ? 0 : 1;
     s_segs = 0ull;
-    s_pool_next = 256;
-    s_alive = 4;
+    s_pool_next = NT;
+    s_alive = NW;
     s_mb_avail = 0;   // (posted, not yet taken: a hint for the waves' exits to the step)
   }
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < NW) {
     s_mb_post[threadIdx.x] = 0;
     s_mb_take[threadIdx.x] = 0;
     s_mb_lim[threadIdx.x] = ka->compact > 0 ? ka->compact : -1;
@@ -706,7 +715,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     constexpr int SZ = static_cast<int>(sizeof(StackT));
     constexpr int W = 16 * SZ;   // words per stack row per wave
     const int i = f * P + p;
-    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_stack) + (i / W) * 256 * SZ + d * 64 * SZ +
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_stack) + (i / W) * NT * SZ + d * 64 * SZ +
                                        (i % W) * 4);
   };
   auto lds_load = [](int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
@@ -774,7 +783,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
     uint64_t freem = ~live;
     bool took = false;
 #pragma unroll 1
-    for (int d = 0; d < 4 && freem; ++d) {
+    for (int d = 0; d < NW && freem; ++d) {
       if (d == wv) continue;
       const int posted = sgpr(lds_load(&s_mb_post[d]));
       if (posted <= sgpr(lds_load(&s_mb_take[d]))) continue;
@@ -1227,7 +1236,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
       StackT* top = stk0;
       // a row of the stack in bytes, held in a register the compiler cannot
       // rematerialise (a literal would be moved into a VGPR on every push)
-      int row_b = 256 * static_cast<int>(sizeof(StackT));
+      int row_b = NT * static_cast<int>(sizeof(StackT));
       asm volatile("" : "+v"(row_b));
       bool go = true;
       while (go) {
@@ -1262,7 +1271,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
           // pop, unconditionally: with an empty stack the top moves one row
           // below the first entry, into the blob's last bytes (a harmless
           // read), and the lane leaves -- one add and one compare, no select
-          top -= 256;
+          top -= NT;
           go = top >= stk0;
           nxt = *top;
         }
@@ -1685,7 +1694,7 @@ __global__ __launch_bounds__(256, min_waves(SCAN, STATS)) void trace_kernel(cons
   // wave timeline (stats variants, or any variant under RTCLJ_TIMELINE in
   // the diagnostic build; NULL otherwise: a uniform branch)
   if (a.dbgw && lane == 0) {
-    const size_t wid = static_cast<size_t>(unit) * 4 + (threadIdx.x >> 6);   // by dispatch slot
+    const size_t wid = static_cast<size_t>(unit) * NW + (threadIdx.x >> 6);   // by dispatch slot
     if (wid < kDbgWaves) {
       a.dbgw[4 * wid + 0] = st_t0;
       a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1727,6 +1736,7 @@ struct Variant {
   int threads = 256;   // workgroup size
 };
 #define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
+#define RT_KW(SRC, SCAN, ST, NW) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST, NW>)
 // The diagnostic library's variants (trace_diag.hip): v's entry, or NULL.
 const Variant* diag_variant(int v);
 

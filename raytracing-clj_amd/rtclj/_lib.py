@@ -86,6 +86,11 @@ SIGNATURES = {
                             C.POINTER(C.c_float), C.c_size_t, C.POINTER(rt_stats)]),
     "rt_render_u8": (C.c_int, [C.POINTER(rt_scene), C.POINTER(rt_camera), C.POINTER(rt_params),
                                C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(rt_stats)]),
+    "rt_render_submit": (C.c_int, [C.POINTER(rt_scene), C.POINTER(rt_camera), C.POINTER(rt_params),
+                                   C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_void_p)]),
+    "rt_render_submit_u8": (C.c_int, [C.POINTER(rt_scene), C.POINTER(rt_camera), C.POINTER(rt_params),
+                                      C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_void_p)]),
+    "rt_render_wait": (C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     "rt_cache_clear": (C.c_int, []),
     "rt_scene_upload": (C.c_int, [C.c_int, C.POINTER(rt_scene), C.POINTER(C.c_void_p)]),
     "rt_scene_free": (C.c_int, [C.c_void_p]),
@@ -107,7 +112,8 @@ SIGNATURES = {
 
 RT_ABI_VERSION = 3   # include/rt.h; the structures above are this revision's
 # functions added within the revision (a build from before them still loads)
-ADDITIVE = {"rt_prepare", "rt_render_u8", "rt_quantize_device"}
+ADDITIVE = {"rt_prepare", "rt_render_u8", "rt_quantize_device", "rt_render_submit", "rt_render_submit_u8",
+            "rt_render_wait"}
 
 
 def load(path: Path) -> C.CDLL:

@@ -120,6 +120,21 @@ def camera(image_width, image_h, vfov, look_from, look_at, vup, defocus_angle, f
     return cam
 
 
+def _frame_args(scene, width, height, spp, max_depth, seed, n_devices, rows, sample_begin, row_tile, flags, out, u8):
+    if not isinstance(scene, Scene):
+        scene = Scene.from_bodies(scene)
+    r0, r1 = (0, height) if rows is None else rows
+    p = rt_params(width=width, height=height, row_begin=r0, row_end=r1, spp=spp, max_depth=max_depth,
+                  seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
+    shape = (max(r1 - r0, 0), width, 3)
+    dt = np.uint8 if u8 else np.float32
+    if out is None:
+        out = np.empty(shape, dt)
+    elif out.shape != shape or out.dtype != dt or not out.flags.c_contiguous:
+        raise ValueError(f"render: out must be C-contiguous {np.dtype(dt).name} {shape}")
+    return scene, p, out
+
+
 def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50, seed: int = 1,
            n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8, stats: dict | None = None,
            flags: int = 0, library=None, out=None, u8: bool = False):
@@ -134,17 +149,8 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
     `u8`: return write-color!'s bytes instead (rt_render_u8: the frame is
     quantised on the device; bit-identical to write_color(render(...)))."""
     dll = library if library is not None else lib
-    if not isinstance(scene, Scene):
-        scene = Scene.from_bodies(scene)
-    r0, r1 = (0, height) if rows is None else rows
-    p = rt_params(width=width, height=height, row_begin=r0, row_end=r1, spp=spp, max_depth=max_depth,
-                  seed=seed, sample_begin=sample_begin, n_devices=n_devices, row_tile=row_tile, flags=flags)
-    shape = (max(r1 - r0, 0), width, 3)
-    dt = np.uint8 if u8 else np.float32
-    if out is None:
-        out = np.empty(shape, dt)
-    elif out.shape != shape or out.dtype != dt or not out.flags.c_contiguous:
-        raise ValueError(f"render: out must be C-contiguous {np.dtype(dt).name} {shape}")
+    scene, p, out = _frame_args(scene, width, height, spp, max_depth, seed, n_devices, rows, sample_begin,
+                                row_tile, flags, out, u8)
     st = rt_stats()
     if u8:
         code = dll.rt_render_u8(C.byref(scene.c), C.byref(cam), C.byref(p), u8ptr(out), out.size, C.byref(st))
@@ -155,6 +161,52 @@ def render(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_d
     if stats is not None:
         stats.update(st.as_dict())
     return out
+
+
+class Frame:
+    """A frame in flight (rt_render_submit): wait() blocks until its rows are
+    in the array and returns it.  Holds the scene, parameters and array until
+    then; a frame dropped unwaited is waited on by its finaliser."""
+
+    def __init__(self, dll, handle, keep, out):
+        self._dll, self._h, self._keep, self.out = dll, handle, keep, out
+
+    def wait(self, stats: dict | None = None):
+        if self._h is None:
+            raise RuntimeError("Frame.wait: already waited on")
+        st = rt_stats()
+        h, self._h = self._h, None
+        code = self._dll.rt_render_wait(h, C.byref(st))
+        self._keep = None
+        if code < 0:
+            raise RTError(code, self._dll.rt_last_error().decode(errors="replace"))
+        if stats is not None:
+            stats.update(st.as_dict())
+        return self.out
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            self._dll.rt_render_wait(self._h, None)
+
+
+def render_async(scene, cam: rt_camera, width: int, height: int, spp: int = 100, max_depth: int = 50,
+                 seed: int = 1, n_devices: int = 0, rows=None, sample_begin: int = 0, row_tile: int = 8,
+                 flags: int = 0, library=None, out=None, u8: bool = False) -> Frame:
+    """render(...) without waiting (rt_render_submit): the devices start on
+    the frame and the call returns a Frame; several frames submitted before
+    the first is waited on run concurrently.  The bits are render's."""
+    dll = library if library is not None else lib
+    scene, p, out = _frame_args(scene, width, height, spp, max_depth, seed, n_devices, rows, sample_begin,
+                                row_tile, flags, out, u8)
+    h = C.c_void_p()
+    if u8:
+        code = dll.rt_render_submit_u8(C.byref(scene.c), C.byref(cam), C.byref(p), u8ptr(out), out.size,
+                                       C.byref(h))
+    else:
+        code = dll.rt_render_submit(C.byref(scene.c), C.byref(cam), C.byref(p), fptr(out), out.size, C.byref(h))
+    if code < 0:
+        raise RTError(code, dll.rt_last_error().decode(errors="replace"))
+    return Frame(dll, h, (scene, cam, p), out)
 
 
 def write_color(lin) -> np.ndarray:
