@@ -145,7 +145,7 @@ def test_submit_errors_and_dropped_frame(gpu_lib):
         R.render_async(sc, cam, 32, 18, spp=1, rows=(10, 40))
     p = rt_params(width=32, height=18, row_begin=0, row_end=18, spp=1, max_depth=5, seed=1, row_tile=8)
     out = np.empty((18, 32, 3), np.float32)
-    code = lib.rt_render_submit(C.byref(R.Scene.from_bodies(sc).c), C.byref(cam), C.byref(p),
+    code = lib.rt_render_submit(C.byref(sc.c), C.byref(cam), C.byref(p),
                                 out.ctypes.data_as(C.POINTER(C.c_float)), out.size, None)
     assert code < 0 and b"NULL frame" in lib.rt_last_error()
     assert lib.rt_render_wait(None, None) < 0 and b"NULL frame" in lib.rt_last_error()
