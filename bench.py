@@ -35,6 +35,7 @@ import ctypes as C
 import json
 import os
 import platform
+import re
 import statistics
 import sys
 import time
@@ -252,6 +253,11 @@ def lib_resolved_variant(scene, device):
     return _resolved[(id(scene), device)]
 
 
+# the product kernel in a rocprofv3 CSV: trace_kernel<SRC, SCAN, false, NW>
+# (the statistics build's STATS = true launches are not the product's)
+PRODUCT_KERNEL = re.compile(r"trace_kernel<[^>]*\bfalse\b")
+
+
 def _pmc_avg(pmc_dir, passes, counters):
     """Per-dispatch averages of PMC counters over the product kernel's
     launches (trace_kernel, not the stats build) in the committed rocprofv3
@@ -262,7 +268,7 @@ def _pmc_avg(pmc_dir, passes, counters):
         if not f.exists():
             return None
         for r in csv.DictReader(open(f)):
-            if "trace_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"] and r["Counter_Name"] in counters:
+            if PRODUCT_KERNEL.search(r["Kernel_Name"]) and r["Counter_Name"] in counters:
                 acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     if any(c not in acc for c in counters):
         return None

@@ -727,47 +727,50 @@ __global__ __launch_bounds__(64 * NW, min_blocks(SCAN, STATS, NW)) void trace_ke
   // finds every sibling gone -- it takes what is left, keeps its own paths,
   // and counts itself back in.
   auto compact_step = [&]() {
+    // (the wave index in an SGPR here: its slots' addresses rebuilt in this
+    // cold step, not held in a VGPR -- at 72 VGPRs one was spilled to scratch)
+    const int wu = static_cast<int>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int P = kargs_opaque()->mb_paths;
     const int leader = static_cast<int>(__builtin_amdgcn_readfirstlane(lane));
     const uint64_t live = __ballot(active);
     const int left = static_cast<int>(__popcll(live));
     bool out = false;   // counted out, and the last wave to do so
     bool post = false;
-    if (left > 0 && left <= sgpr(lds_load(&s_mb_lim[wv]))) {
+    if (left > 0 && left <= sgpr(lds_load(&s_mb_lim[wu]))) {
       post = sgpr(lds_load(&s_alive)) > 1;
       // posting now; or alone (no sibling will ever take them): not again
-      if (lane == leader) __hip_atomic_store(&s_mb_lim[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == leader) __hip_atomic_store(&s_mb_lim[wu], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (left == 0 || post) {
       if (post) {
         const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(live >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(live), 0u)));
         if (active) {
-          *mb_word(wv, 0, rank, P) = __float_as_uint(ox);
-          *mb_word(wv, 1, rank, P) = __float_as_uint(oy);
-          *mb_word(wv, 2, rank, P) = __float_as_uint(oz);
-          *mb_word(wv, 3, rank, P) = __float_as_uint(dx);
-          *mb_word(wv, 4, rank, P) = __float_as_uint(dy);
-          *mb_word(wv, 5, rank, P) = __float_as_uint(dz);
-          *mb_word(wv, 6, rank, P) = __float_as_uint(tr);
-          *mb_word(wv, 7, rank, P) = __float_as_uint(tg);
-          *mb_word(wv, 8, rank, P) = __float_as_uint(tb);
-          *mb_word(wv, 9, rank, P) = st;
-          *mb_word(wv, 10, rank, P) = static_cast<uint32_t>(q);
-          *mb_word(wv, 11, rank, P) = static_cast<uint32_t>(rem);
-          *mb_word(wv, 12, rank, P) = static_cast<uint32_t>(last);
+          *mb_word(wu, 0, rank, P) = __float_as_uint(ox);
+          *mb_word(wu, 1, rank, P) = __float_as_uint(oy);
+          *mb_word(wu, 2, rank, P) = __float_as_uint(oz);
+          *mb_word(wu, 3, rank, P) = __float_as_uint(dx);
+          *mb_word(wu, 4, rank, P) = __float_as_uint(dy);
+          *mb_word(wu, 5, rank, P) = __float_as_uint(dz);
+          *mb_word(wu, 6, rank, P) = __float_as_uint(tr);
+          *mb_word(wu, 7, rank, P) = __float_as_uint(tg);
+          *mb_word(wu, 8, rank, P) = __float_as_uint(tb);
+          *mb_word(wu, 9, rank, P) = st;
+          *mb_word(wu, 10, rank, P) = static_cast<uint32_t>(q);
+          *mb_word(wu, 11, rank, P) = static_cast<uint32_t>(rem);
+          *mb_word(wu, 12, rank, P) = static_cast<uint32_t>(last);
         }
       }
       int old = 0;
       if (lane == leader) {
         if (post) {
-          __hip_atomic_store(&s_mb_post[wv], left, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&s_mb_post[wu], left, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           atomicAdd(&s_mb_avail, left);
         }
         old = __hip_atomic_fetch_add(&s_alive, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         // the last one out withdraws its post (no sibling is left to take any of it)
         if (post && old <= 1) {
-          __hip_atomic_store(&s_mb_post[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&s_mb_post[wu], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           atomicAdd(&s_mb_avail, -left);
         }
       }
@@ -784,7 +787,7 @@ __global__ __launch_bounds__(64 * NW, min_blocks(SCAN, STATS, NW)) void trace_ke
     bool took = false;
 #pragma unroll 1
     for (int d = 0; d < NW && freem; ++d) {
-      if (d == wv) continue;
+      if (d == wu) continue;
       const int posted = sgpr(lds_load(&s_mb_post[d]));
       if (posted <= sgpr(lds_load(&s_mb_take[d]))) continue;
       const int want = static_cast<int>(__popcll(freem));
@@ -1694,7 +1697,9 @@ __global__ __launch_bounds__(64 * NW, min_blocks(SCAN, STATS, NW)) void trace_ke
   // wave timeline (stats variants, or any variant under RTCLJ_TIMELINE in
   // the diagnostic build; NULL otherwise: a uniform branch)
   if (a.dbgw && lane == 0) {
-    const size_t wid = static_cast<size_t>(unit) * NW + (threadIdx.x >> 6);   // by dispatch slot
+    // (by dispatch slot; the wave index rebuilt here, in an SGPR: held from
+    // the start in a VGPR, at 72 VGPRs it was spilled to scratch)
+    const size_t wid = static_cast<size_t>(unit) * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wid < kDbgWaves) {
       a.dbgw[4 * wid + 0] = st_t0;
       a.dbgw[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();

@@ -6,6 +6,7 @@ launches, plus the derived VALU / occupancy / HBM figures bench.py reports.
   python tools/pmc_summary.py profiles/r02/pmc_c1 [kernel_stats.csv]
 """
 import csv
+import re
 import statistics
 import sys
 from pathlib import Path
@@ -16,7 +17,7 @@ def main():
     acc = {}
     for f in sorted(d.glob("*.csv")):
         for r in csv.DictReader(open(f)):
-            if "trace_kernel" in r["Kernel_Name"] and "false>" in r["Kernel_Name"]:
+            if re.search(r"trace_kernel<[^>]*\bfalse\b", r["Kernel_Name"]):
                 acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     # the median launch, as bench.py takes it (the timed frames' recorded order)
     avg = {k: statistics.median(v) for k, v in acc.items()}
