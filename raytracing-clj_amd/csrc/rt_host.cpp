@@ -367,8 +367,9 @@ HostPool* g_pool = new HostPool;   // never destroyed (workers may still wait on
 constexpr int kSceneCache = 4;   // scenes kept per device (least recently used out)
 // idle contexts kept per device: as many as a scene has per-stream schedule
 // slots (trace.hip kSchedStreams), so RT_FLAG_SHARDS_ON_DEVICE0 with 8 shards
-// keeps its 8 streams and their tile orders from call to call
-constexpr int kFreeCtx = 8;
+// and two frames in flight (rt_render_submit) keeps its 16 streams and their
+// tile orders from call to call
+constexpr int kFreeCtx = 16;
 
 struct DeviceCache {
   std::mutex mu;

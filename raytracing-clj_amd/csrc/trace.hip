@@ -301,7 +301,7 @@ struct Schedule {
   int units_cap = 0;
   int plan_units = -1;                  // the plan's unit count (-1: none)
 };
-constexpr int kSchedStreams = 8;
+constexpr int kSchedStreams = 16;
 struct ScheduleSet {
   std::mutex mu;
   int used = 0;
