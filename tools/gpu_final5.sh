@@ -23,6 +23,11 @@ for s in $STEPS; do
            tail -1 $OUT/dist2.log > $OUT/dist2.json ;;
     dist8) step dist8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 10 --warmup 3 --cpu-baseline off
            tail -1 $OUT/dist8.log > $OUT/dist8.json ;;
+    configs) for c in c2 c3 c4; do
+               extra=""; [ "$c" = "c4" ] && extra="--steps 2 --warmup 1 --pipelined off"
+               step $c 500 python bench.py --cpu-baseline off --e2e off --workload $c $extra
+               tail -1 $OUT/$c.log > $OUT/$c.json
+             done ;;
     shard) step shard 400 python tools/shard_time.py --workload c1 --reps 9 --inflight 2 --frames 80
            grep "N=" $OUT/shard.log ;;
   esac
