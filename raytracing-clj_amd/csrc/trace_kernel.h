@@ -355,20 +355,19 @@ struct alignas(16) KNode {
 };
 static_assert(sizeof(KNode) == 80, "KNode layout");
 
-// The pool tile: 8 x 8 pixels per 256-thread workgroup
 // The pool tile: 8 pixels wide, 8 rows high -- 4 for the 8-body-leaf
 // traversal, whose large-scene LDS image (C4: 1000 bodies) needs the 768 B
-// that half the pixel sums give back to stay at 5 workgroups per CU
+// that half the pixel sums give back (its 512-thread workgroups: 3 per CU)
 constexpr int kTile = 8;
 // the 4-body tree's leaf record in LDS: two pairs and their index pairs
 constexpr int kLeafRecBytes = 80;
 constexpr int kPoolPx = kTile * kTile;
 constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_BVHS ? 16 : kTile; }
 
-// Waves per SIMD the register allocator must leave room for: six for the
-// default traversal (80 VGPRs; its 26.5 KB LDS image fits 6 workgroups per
-// CU), five for the 8-body-leaf one (C4: its LDS allows 5 workgroups per
-// CU).  Without the bound the unit loop's longer-lived uniform values
+// Waves per SIMD the register allocator must leave room for: seven for the
+// compact image (72 VGPRs; 23.0 KB of LDS fits 7 workgroups per CU), six
+// for the 4-body traversal (80 VGPRs; 26.6 KB) and for the 8-body-leaf one
+// (C4: 8-wave workgroups, 3 per CU by its 33.6 KB of LDS).  Without the bound the unit loop's longer-lived uniform values
 // (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
 // waves; with it, a few of them spill to scratch outside the hot loop.
 constexpr int min_waves(int scan, bool stats) {
