@@ -291,27 +291,30 @@ int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_s
  * 4-body tree's LDS image would cap a CU below 5 workgroups and the 8-body
  * tree's is smaller);
  * 16 = BVH traversal, 4 bodies per leaf, nodes and leaf bodies in LDS;
- * 18 = the same with 8 bodies per leaf; 22 = 16 in a compact LDS image (u8
- * node-index stack, u32 pixel sums: seven workgroups per CU; 0 selects it
- * wherever spp <= 255, every albedo lies in [-1, 1] and the tree has <= 256
- * nodes, else 16); 12 = BVH with 2 bodies per leaf read
- * from global memory (the fallback for a tree too big for LDS); 5 = linear
- * scan, bodies in groups of 4 through the scalar cache (the fallback for a
- * tree too deep for the stack).  The diagnostic build lib/librtclj_diag.so
- * (make diag) adds: 1 / 2 = simple scan, table in LDS / scalar cache;
- * 4 = grouped scan, table in LDS (north_star's LDS-staged sphere list);
- * 8 / 9 = packed-fp32 scan, LDS / scalar; 11 = BVH in LDS, 2 bodies per leaf;
- * 14 = 11 with a speculative while-while traversal; and the statistics builds
- * 3, 6, 7, 10, 13, 15, 17, 19 (= 1, 4, 5, 9, 11, 14, 16, 18 with wave-level
- * counters, rt_debug_stats).  Returns the previous value, or RT_E_ARG for a
- * variant this build does not hold.  Applies to subsequent launches in this
+ * 18 = the same with 8 bodies per leaf, in 512-thread workgroups (one LDS
+ * image per 8 waves); 22 = 16 in a compact LDS image (u8 node-index stack,
+ * u32 pixel sums that count their wraps above 255 spp: seven workgroups per
+ * CU; 0 selects it wherever spp < 65536, every albedo lies in [-1, 1], the
+ * tree has <= 256 nodes and no frame side exceeds 65536, else 16); 12 = BVH
+ * with 2 bodies per leaf read from global memory (the fallback for a tree
+ * too big for LDS); 5 = linear scan, bodies in groups of 4 through the
+ * scalar cache (the fallback for a tree too deep for the stack).  The
+ * diagnostic build lib/librtclj_diag.so (make diag) adds: 1 / 2 = simple
+ * scan, table in LDS / scalar cache; 4 = grouped scan, table in LDS
+ * (north_star's LDS-staged sphere list); 8 / 9 = packed-fp32 scan, LDS /
+ * scalar; 11 = BVH in LDS, 2 bodies per leaf; 20 / 21 = direction-sorted
+ * 8-wave lock-step workgroups (octant sort / live-path packing); and the
+ * statistics builds 3, 6, 7, 10, 13, 17, 19 (= 1, 4, 5, 9, 11, 16, 18 with
+ * wave-level counters, rt_debug_stats).  Returns the previous value, or
+ * RT_E_ARG for a variant this build does not hold.  Applies to subsequent
+ * launches in this
  * process (an atomic, read once per launch). */
 int rt_set_variant(int variant);
 
 /* The kernel variant the current selector resolves to for ds (the default
  * resolved for this scene, or a fallback when a tree does not fit), before
  * the per-launch choice between 16 and its compact image 22, which also
- * depends on the launch (spp <= 255, frame size): rt_launch_occupancy's
+ * depends on the launch (spp < 65536, frame size): rt_launch_occupancy's
  * out4[3] reports the variant a given launch runs.  For reading the matching
  * statistics build.  -1 on a NULL scene. */
 int rt_resolve_variant(const rt_dscene* ds);
