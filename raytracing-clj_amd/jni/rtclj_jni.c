@@ -12,6 +12,9 @@
  *                                     float[] outRgb);   // RT_FLAG_REALM: -M:realm
  *   static native int renderBytes(... the same ..., int nGpus, int flags,
  *                                 byte[] outRgb);   // rt_render_u8: write-color!'s bytes
+ *   static native long submitBytes(... the same ..., int nGpus, int flags);
+ *                                 // rt_render_submit_u8: a frame in flight, its handle
+ *   static native int waitBytes(long frame, byte[] outRgb);   // rt_render_wait
  *   static native int cameraSetup(int width, int height, double vfov,
  *                                 double[] lookFrom, double[] lookAt, double[] vup,
  *                                 double defocusAngle, double focusDist,
@@ -47,11 +50,22 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_deviceCount(JNIEnv* env, jclass cls) {
   return rt_device_count();
 }
 
-/* out_rgb: a float[] (rt_render) or, u8, a byte[] (rt_render_u8) */
+/* A frame in flight (submitBytes .. waitBytes): rt_render_submit_u8's frame
+ * and the shim's buffer it renders into (the Java array is filled at the
+ * wait: nothing is pinned while the devices work). */
+typedef struct {
+  rt_frame* frame;
+  uint8_t* buf;
+  size_t len;
+} JFrame;
+
+/* out_rgb: a float[] (rt_render) or, u8, a byte[] (rt_render_u8); submit
+ * (non-NULL): rt_render_submit_u8 into a buffer of the shim's, *submit = its
+ * JFrame (out_rgb unused) */
 static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloatArray mats, jfloatArray camera,
                         jint defocus, jint width, jint height, jint spp, jint depth, jlong seed, jint n_gpus,
-                        jint flags, jarray out_rgb, int u8) {
-  if (!spheres || !kinds || !mats || !camera || !out_rgb) { /* Java nulls */
+                        jint flags, jarray out_rgb, int u8, JFrame** submit) {
+  if (!spheres || !kinds || !mats || !camera || (!out_rgb && !submit)) { /* Java nulls */
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
   }
@@ -65,7 +79,7 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   /* The frame is width x height x 3 floats (bytes); a longer Java array keeps its
    * tail (only the frame is copied back), a shorter one is an argument error
    * raised before anything is rendered. */
-  if (width <= 0 || height <= 0 || (*env)->GetArrayLength(env, out_rgb) / 3 / width < height) {
+  if (width <= 0 || height <= 0 || (!submit && (*env)->GetArrayLength(env, out_rgb) / 3 / width < height)) {
     throw_rt(env, RT_E_ARG);
     return RT_E_ARG;
   }
@@ -113,7 +127,24 @@ static jint render_impl(JNIEnv* env, jfloatArray spheres, jintArray kinds, jfloa
   p.seed = (uint64_t)seed;
   p.n_devices = n_gpus;
   p.flags = flags;
-  if (u8) {
+  if (submit) {   /* the buffer goes to the JFrame (freed at the wait) */
+    JFrame* jf = (JFrame*)malloc(sizeof(JFrame));
+    if (!jf) {
+      jclass oom = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+      if (oom) (*env)->ThrowNew(env, oom, "rtclj submit: cannot allocate the frame");
+      rc = RT_E_ALLOC;
+      goto done;
+    }
+    jf->buf = (uint8_t*)out;
+    jf->len = frame;
+    rc = rt_render_submit_u8(&scene, &cam, &p, jf->buf, frame, &jf->frame);
+    if (rc >= 0) {
+      *submit = jf;
+      out = NULL;
+    } else {
+      free(jf);
+    }
+  } else if (u8) {
     rc = rt_render_u8(&scene, &cam, &p, (uint8_t*)out, frame, NULL);
     if (rc >= 0) (*env)->SetByteArrayRegion(env, out_rgb, 0, (jsize)frame, (const jbyte*)out);
   } else {
@@ -135,7 +166,7 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_render(JNIEnv* env, jclass cls, jfloatA
                                                 jfloatArray out_rgb) {
   (void)cls;
   return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, 0,
-                     out_rgb, 0);
+                     out_rgb, 0, NULL);
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls, jfloatArray spheres,
@@ -145,7 +176,7 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_renderWithFlags(JNIEnv* env, jclass cls
                                                          jfloatArray out_rgb) {
   (void)cls;
   return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, flags,
-                     out_rgb, 0);
+                     out_rgb, 0, NULL);
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_renderBytes(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
@@ -154,7 +185,49 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_renderBytes(JNIEnv* env, jclass cls, jf
                                                      jint flags, jbyteArray out_rgb) {
   (void)cls;
   return render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus, flags,
-                     out_rgb, 1);
+                     out_rgb, 1, NULL);
+}
+
+/* Frames in flight for a host drawing a sequence of frames: submitBytes
+ * returns once the frame is on the devices (0 and a pending exception on
+ * error); waitBytes blocks until it is rendered, copies its bytes into
+ * outRgb (>= width x height x 3; a longer array keeps its tail) and frees
+ * the handle -- every handle is waited on exactly once, from any thread. */
+JNIEXPORT jlong JNICALL Java_rtclj_Native_submitBytes(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
+                                                      jfloatArray mats, jfloatArray camera, jint defocus, jint width,
+                                                      jint height, jint spp, jint depth, jlong seed, jint n_gpus,
+                                                      jint flags) {
+  (void)cls;
+  JFrame* jf = NULL;
+  const jint rc = render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus,
+                              flags, NULL, 1, &jf);
+  return rc >= 0 ? (jlong)(intptr_t)jf : 0;
+}
+
+JNIEXPORT jint JNICALL Java_rtclj_Native_waitBytes(JNIEnv* env, jclass cls, jlong frame, jbyteArray out_rgb) {
+  (void)cls;
+  if (!frame) {
+    throw_rt(env, RT_E_ARG);
+    return RT_E_ARG;
+  }
+  JFrame* jf = (JFrame*)(intptr_t)frame;
+  int rc = rt_render_wait(jf->frame, NULL);   /* (the frame is consumed either way) */
+  int short_out = 0;
+  if (rc >= 0) {
+    if (!out_rgb || (size_t)(*env)->GetArrayLength(env, out_rgb) < jf->len)
+      short_out = 1;
+    else
+      (*env)->SetByteArrayRegion(env, out_rgb, 0, (jsize)jf->len, (const jbyte*)jf->buf);
+  }
+  free(jf->buf);
+  free(jf);
+  if (short_out) {   /* (the frame is gone: an argument error of the wait) */
+    jclass ex = (*env)->FindClass(env, "java/lang/RuntimeException");
+    if (ex) (*env)->ThrowNew(env, ex, "rt error -1: waitBytes: outRgb is null or shorter than the frame");
+    return RT_E_ARG;
+  }
+  if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_rt(env, rc);
+  return rc;
 }
 
 /* -main's camera let block (raytracing.clj:105-139) through rt_camera_setup:

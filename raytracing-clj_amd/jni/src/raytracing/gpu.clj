@@ -59,6 +59,28 @@
                         (if realm? Native/FLAG_REALM 0) out)
     out))
 
+(defn submit-bytes
+  "render-bytes without waiting (rt_render_submit_u8): returns a frame in
+  flight for await-bytes.  A host drawing a sequence of frames submits the
+  next before it awaits the last, as the executor's futures do
+  (raytracing.clj:157-171)."
+  [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
+   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
+  (let [[sph knd mat] (flatten-bodies bodies)
+        cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))]
+    {:handle (Native/submitBytes sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
+                                 samples-per-px max-depth (long seed) (int gpus)
+                                 (if realm? Native/FLAG_REALM 0))
+     :size (* width height 3)}))
+
+(defn await-bytes
+  "The bytes of a frame from submit-bytes (rt_render_wait); each frame is
+  awaited exactly once."
+  [{:keys [handle size]}]
+  (let [out (byte-array size)]
+    (Native/waitBytes handle out)
+    out))
+
 (defn camera
   "-main's camera values (raytracing.clj:105-139) through rt_camera_setup, in
   the keys render takes."

@@ -25,6 +25,14 @@ public final class Native {
                                        int width, int height, int spp, int depth, long seed, int nGpus, int flags,
                                        byte[] outRgb);
 
+  /** renderBytes without waiting (rt_render_submit_u8): a frame in flight; returns its handle. */
+  public static native long submitBytes(float[] spheres, int[] kinds, float[] mats, float[] camera, int defocus,
+                                        int width, int height, int spp, int depth, long seed, int nGpus,
+                                        int flags);
+
+  /** Waits for a submitted frame (rt_render_wait), copies its bytes into outRgb, frees the handle. */
+  public static native int waitBytes(long frame, byte[] outRgb);
+
   /** -main's camera values (rt_camera_setup) into outCamera[18]; returns the defocus flag. */
   public static native int cameraSetup(int width, int height, double vfov, double[] lookFrom, double[] lookAt,
                                        double[] vup, double defocusAngle, double focusDist, float[] outCamera);

@@ -63,6 +63,10 @@ def _load():
                                                      VP]
     d.Java_rtclj_Native_renderBytes.restype = i32
     d.Java_rtclj_Native_renderBytes.argtypes = [VP, VP, VP, VP, VP, VP, i32, i32, i32, i32, i32, i64, i32, i32, VP]
+    d.Java_rtclj_Native_submitBytes.restype = i64
+    d.Java_rtclj_Native_submitBytes.argtypes = [VP, VP, VP, VP, VP, VP, i32, i32, i32, i32, i32, i64, i32, i32]
+    d.Java_rtclj_Native_waitBytes.restype = i32
+    d.Java_rtclj_Native_waitBytes.argtypes = [VP, VP, i64, VP]
     d.Java_rtclj_Native_cameraSetup.restype = i32
     d.Java_rtclj_Native_cameraSetup.argtypes = [VP, VP, i32, i32, C.c_double, VP, VP, VP, C.c_double, C.c_double, VP]
     d.Java_rtclj_Native_writePpm.restype = i32
@@ -234,6 +238,32 @@ def test_render_bytes_checks_and_errors(jni):
     assert np.all(read_b(d, out, w * h * 3) == 9)
 
 
+def test_submit_wait_checks_and_errors(jni):
+    """submitBytes / waitBytes (frames in flight): a null input is an
+    argument error before any copy; a well-formed submit maps
+    rt_render_submit_u8's status (no GPU here: RT_E_NODEV, handle 0) with
+    every copy released; waitBytes(0) is an argument error."""
+    import rtclj
+    d = jni
+    env = d.mock_env()
+    sc, cam, w, h, (sph, knd, mat, c18) = _scene_args(d)
+    hd = d.Java_rtclj_Native_submitBytes(env, None, None, knd, mat, c18, cam.defocus, w, h, 4, 50, 1, 1, 0)
+    st = stats(d)
+    assert hd == 0 and st["pending"] and clean(st) and st["gets"] == 0, st
+    d.mock_clear_exception()
+    rc = d.Java_rtclj_Native_waitBytes(env, None, 0, barr(d, np.zeros(w * h * 3)))
+    assert rc == RT_E_ARG and stats(d)["pending"]
+    d.mock_clear_exception()
+    hd = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 4, 50, 1, 1, 0)
+    st = stats(d)
+    assert clean(st) and st["gets"] == 3, st
+    if rtclj.lib.rt_device_count() > 0:
+        assert hd != 0 and not st["pending"]
+        assert d.Java_rtclj_Native_waitBytes(env, None, hd, barr(d, np.zeros(w * h * 3))) == 0
+        return
+    assert hd == 0 and st["pending"] and d.mock_exception_message().startswith(b"rt error -5: ")
+
+
 def test_camera_setup_equals_rt_camera_setup(jni):
     from rtclj import raytracing as R
     d = jni
@@ -352,3 +382,24 @@ def test_shim_render_equals_rt_render(gpu_lib, jni):
         gb = read_b(d, ob, n + 3)
         assert np.array_equal(gb[:n].reshape(h, w, 3), R.write_color(ref))
         assert np.all(gb[n:] == 9)
+        # submitBytes / waitBytes: two frames in flight, waited on in reverse;
+        # each equals renderBytes' bytes; a short array at the wait throws
+        env = d.mock_env()
+        h1 = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 8, 50, 3, 1,
+                                             flags or 0)
+        h2 = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 8, 50, 4, 1,
+                                             flags or 0)
+        assert h1 and h2 and not stats(d)["pending"]
+        o2 = barr(d, np.full(n, 9))
+        assert d.Java_rtclj_Native_waitBytes(env, None, h2, o2) == 0
+        ref4 = R.render(sc, cam, w, h, spp=8, max_depth=50, seed=4, flags=flags or 0)
+        assert np.array_equal(read_b(d, o2, n).reshape(h, w, 3), R.write_color(ref4))
+        o1 = barr(d, np.full(n + 3, 9))
+        assert d.Java_rtclj_Native_waitBytes(env, None, h1, o1) == 0
+        g1 = read_b(d, o1, n + 3)
+        assert np.array_equal(g1[:n].reshape(h, w, 3), R.write_color(ref)) and np.all(g1[n:] == 9)
+        h3 = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 8, 50, 3, 1,
+                                             flags or 0)
+        assert d.Java_rtclj_Native_waitBytes(env, None, h3, barr(d, np.zeros(n - 1))) == RT_E_ARG
+        assert stats(d)["pending"] and clean(stats(d))
+        d.mock_clear_exception()
