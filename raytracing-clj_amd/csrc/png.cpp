@@ -128,7 +128,9 @@ bool deflate_chunked(const std::vector<uint8_t>& raw, std::vector<uint8_t>* z) {
   parallel_for(nchunk, [&](int c) {
     const size_t b = static_cast<size_t>(c) * kChunk, len = std::min(kChunk, n - b);
     z_stream zs{};
-    if (deflateInit2(&zs, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+    // level 1: a C1 frame in ~1/2.5 of level 6's time for a 13 % larger file
+    // (the bytes are a lossless encoding either way; the pixels are the PPM's)
+    if (deflateInit2(&zs, 1, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
       ok = false;
       return;
     }
