@@ -580,7 +580,7 @@ static size_t lds_of_compact(const DTree& t) {
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
 // kernel's static LDS (pool counter, the 64 pixels' colour sums and pixel
 // table).  (Its registers allow 6; C1's 24.0 KB image fits 6 as well.)
-constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal's 8x4 tile, no table: 1.8 KB less)
+constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal: no table, 1 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 
 // selector -> the variant a launch on ds runs

@@ -355,14 +355,15 @@ struct alignas(16) KNode {
 };
 static_assert(sizeof(KNode) == 80, "KNode layout");
 
-// The pool tile: 8 pixels wide, 8 rows high -- 4 for the 8-body-leaf
-// traversal, whose large-scene LDS image (C4: 1000 bodies) needs the 768 B
-// that half the pixel sums give back (its 512-thread workgroups: 3 per CU)
+// The pool tile: 8 x 8 pixels.  (The 8-body-leaf traversal ran 8 x 4 tiles
+// while its 256-thread workgroups were LDS-bound at 5 per CU; in 512-thread
+// workgroups, 3 per CU by registers, the 8 x 8 pool's longer workgroup
+// lifetimes are worth 1 %: C4 4.95 vs 4.99 s, profiles/r05/c4_tile/)
 constexpr int kTile = 8;
 // the 4-body tree's leaf record in LDS: two pairs and their index pairs
 constexpr int kLeafRecBytes = 80;
 constexpr int kPoolPx = kTile * kTile;
-constexpr int tile_rows(int scan) { return scan == SCAN_BVHO ? 4 : scan == SCAN_BVHS ? 16 : kTile; }
+constexpr int tile_rows(int scan) { return scan == SCAN_BVHS ? 16 : kTile; }
 
 // Waves per SIMD the register allocator must leave room for: seven for the
 // compact image (72 VGPRs; 23.0 KB of LDS fits 7 workgroups per CU), six

@@ -16,7 +16,7 @@ fp64 reference-semantics pin of the benchmark workload.
   C4 7680x4320, 2000 spp, depth 64, 1000 bodies: the whole frame's
      properties, a row band re-rendered alone equal to the frame's rows, and
      eight 64-pixel strips bit-exact against the mirror at full spp; and C4's own
-     kernel (8-body leaves, u8 stack, 8x4 tiles) on every 270th row against
+     kernel (8-body leaves, u8 stack, 512-thread workgroups) on every 270th row against
      MODE_REF64 at 16 spp (the cover pin's bounds, as for C1).
 
 Every full frame's segments per sample (one hit-anything call each,
@@ -187,7 +187,7 @@ def test_c4_full_frame(gpu_lib):
 
 def test_c4_against_fp64_reference_semantics(gpu_lib):
     """C4's kernel instantiation -- 1000 bodies, depth 64, the 8-body-leaf
-    tree (u8 stack), 8x4-pixel pools, the r = 1000 ground's self-hit guard at
+    tree (u8 stack), 8x8-pixel pools, the r = 1000 ground's self-hit guard at
     depth 64 -- against the Clojure path in double (hittable.clj:10-23,
     raytracing.clj:45-58) on rows 0, 270, ..., 4050 of the 7680x4320 frame at
     16 spp (reduced from 2000 so that MODE_REF64's linear scan over 1000
