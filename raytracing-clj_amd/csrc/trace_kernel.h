@@ -368,7 +368,7 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHS ? 16 : kTile; }
 // Waves per SIMD the register allocator must leave room for: seven for the
 // compact image (72 VGPRs; 23.0 KB of LDS fits 7 workgroups per CU), six
 // for the 4-body traversal (80 VGPRs; 26.6 KB) and for the 8-body-leaf one
-// (C4: 8-wave workgroups, 3 per CU by its 33.6 KB of LDS).  Without the bound the unit loop's longer-lived uniform values
+// (C4: 8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).  Without the bound the unit loop's longer-lived uniform values
 // (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
 // waves; with it, a few of them spill to scratch outside the hot loop.
 constexpr int min_waves(int scan, bool stats) {
