@@ -368,16 +368,17 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHS ? 16 : kTile; }
 // Waves per SIMD the register allocator must leave room for: seven for the
 // compact image (72 VGPRs; 23.0 KB of LDS fits 7 workgroups per CU), six
 // for the 4-body traversal (80 VGPRs; 26.6 KB) and for the 8-body-leaf one
-// (C4: 8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).  Without the bound the unit loop's longer-lived uniform values
-// (SGPRs at their limit, copied into VGPRs) take it to ~100 VGPRs and four
-// waves; with it, a few of them spill to scratch outside the hot loop.
+// (C4: 8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).
+// Without the bound the unit loop's longer-lived uniform values (SGPRs at
+// their limit, copied into VGPRs) take it to ~100 VGPRs and four waves; with
+// it, a few of them spill to scratch outside the hot loop.  HIP passes
+// __launch_bounds__'s second argument on as amdgpu_waves_per_eu: a count of
+// waves per SIMD, whatever the workgroup's size.  The 8-body-leaf kernel asks
+// for 3 (a register budget of 168): it allocates 75 VGPRs either way, and
+// the schedule made under 3 is C4's faster one -- 4.996 vs 5.019 s with 6
+// asked, same box (profiles/r05/launch_bound/).
 constexpr int min_waves(int scan, bool stats) {
-  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 6 : 1;
-}
-// __launch_bounds__'s minimum workgroups per CU for that many waves per SIMD
-// with NW-wave workgroups (4 SIMDs a CU)
-constexpr int min_blocks(int scan, bool stats, int nw) {
-  return (min_waves(scan, stats) * 4 + nw - 1) / nw;
+  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 3 : 1;
 }
 
 // The diagnostic scans (SCAN_SIMPLE, SCAN_PK4: the linear scans of the A/B
@@ -391,7 +392,7 @@ __device__ void diag_scan(const struct KArgs& a, const float4* s_geo, float ox, 
 // image one workgroup of 8 waves shares: 3 workgroups = 6 waves per SIMD on
 // C4's 1000-body tree, where 4-wave workgroups fit 5 per CU = 5 waves)
 template <int SRC, int SCAN, bool STATS = false, int NW = 4>
-__global__ __launch_bounds__(64 * NW, min_blocks(SCAN, STATS, NW)) void trace_kernel(const KArgs a) {
+__global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS)) void trace_kernel(const KArgs a) {
   constexpr int NT = 64 * NW;   // threads
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
   // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample

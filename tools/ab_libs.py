@@ -29,37 +29,42 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variants", nargs="+", type=int, default=None,
+                    help="per --libs entry: its bench.py --variant (default 0 for every one)")
     a = ap.parse_args(argv)
-    res = {lib: [] for lib in a.libs}
-    res_plain = {lib: [] for lib in a.libs}   # dispatch_order: the frame in plain tile order
+    variants = a.variants or [0] * len(a.libs)
+    assert len(variants) == len(a.libs), "--variants: one per --libs entry"
+    runs = [(lib, v, f"{Path(lib).name}:v{v}" if v else Path(lib).name) for lib, v in zip(a.libs, variants)]
+    res = {name: [] for _, _, name in runs}
+    res_plain = {name: [] for _, _, name in runs}   # dispatch_order: the frame in plain tile order
     out = open(a.out, "a") if a.out else None
     for r in range(a.rounds):
-        for lib in a.libs:
+        for lib, v, name in runs:
             env = dict(os.environ, RTCLJ_LIBRARY=str(Path(lib).resolve()))
             cmd = [sys.executable, str(ROOT / "bench.py"), "--cpu-baseline", "off", "--steps", str(a.steps),
-                   "--warmup", "2"] + extra
+                   "--warmup", "2", "--variant", str(v)] + extra
             p = subprocess.run(["timeout", "-k", "10", "240"] + cmd, env=env, capture_output=True, text=True)
             if p.returncode != 0:
                 print(f"run failed ({p.returncode}) for {lib}:\n{p.stderr[-3000:]}", flush=True)
                 sys.exit(p.returncode)
             line = json.loads(p.stdout.strip().splitlines()[-1])
             ms = line["kernel_ms_avg"]
-            res[lib].append(ms)
+            res[name].append(ms)
             plain = (line.get("dispatch_order") or {}).get("kernel_ms")
             if plain is not None:
-                res_plain[lib].append(plain)
-            print(f"round {r} {Path(lib).name:24s} kernel {ms:.3f} ms  plain order {plain}  "
+                res_plain[name].append(plain)
+            print(f"round {r} {name:24s} kernel {ms:.3f} ms  plain order {plain}  "
                   f"{line['value']:.0f} Msamples/s", flush=True)
             if out:
-                out.write(json.dumps({"round": r, "lib": Path(lib).name, "kernel_ms_avg": ms,
+                out.write(json.dumps({"round": r, "lib": name, "kernel_ms_avg": ms, "occupancy": line.get("occupancy"),
                                       "value": line["value"], "bvh": line.get("bvh_per_segment"),
                                       "plain_ms": plain,
                                       "args": extra}) + "\n")
                 out.flush()
-    for lib, v in res.items():
-        print(f"{Path(lib).name:24s} median {statistics.median(v):.3f} ms  min {min(v):.3f}  runs {v}")
-        if res_plain[lib]:
-            print(f"{Path(lib).name:24s} plain order median {statistics.median(res_plain[lib]):.3f} ms")
+    for name, v in res.items():
+        print(f"{name:24s} median {statistics.median(v):.3f} ms  min {min(v):.3f}  runs {v}")
+        if res_plain[name]:
+            print(f"{name:24s} plain order median {statistics.median(res_plain[name]):.3f} ms")
 
 
 if __name__ == "__main__":
