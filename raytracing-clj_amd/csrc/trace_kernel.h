@@ -57,6 +57,7 @@
 #include <vector>
 
 #include "bvh.h"
+#include "fp_rn.h"
 #include "rt_internal.h"
 
 namespace rtclj {
@@ -152,22 +153,6 @@ __device__ __forceinline__ float rng_uniform(uint32_t& s) {
   return static_cast<float>(s >> 8) * 0x1p-24f;
 }
 
-// Correctly rounded sqrt, the same bits as sqrtf for every input: for
-// x >= 2^-96 (every normal case here) the hardware v_sqrt_f32 corrected by
-// the residuals of its neighbours -- the sequence the compiler emits for
-// sqrtf, without its denormal scaling and zero/inf class fix-up (a rare
-// branch keeps those for tiny, NaN and negative inputs): 16 -> 9 VALU.
-__device__ __forceinline__ float sqrt_rn(float x) {
-  if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
-  const float s = __builtin_amdgcn_sqrtf(x);
-  const int si = __builtin_bit_cast(int, s);
-  const float sd = __builtin_bit_cast(float, si - 1), su = __builtin_bit_cast(float, si + 1);
-  const float rd = fmaf(-sd, s, x), ru = fmaf(-su, s, x);
-  float r = rd <= 0.0f ? sd : s;
-  r = ru > 0.0f ? su : r;
-  return r;
-}
-
 // xi - 0.5 (compute-pixel's jitter, raytracing.clj:145-146), exact in fp32
 __device__ __forceinline__ float rng_centered(uint32_t& s) {
   s ^= s << 13;
@@ -215,7 +200,9 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
     } while (!(l2 <= 1.0f));
     asm volatile("" : "+v"(l2));   // (keeps the two loops apart: one test a trip)
   } while (__builtin_expect(!(l2 > 0.0f), 0));
-  const float il = 1.0f / sqrt_rn(l2);   // contract: v * (1/|v|)
+  // contract: v * (1/|v|); the components are multiples of 2^-23, so
+  // 2^-46 <= l2 <= 1 and |v| lies in rcp_rn_normal's range
+  const float il = rcp_rn_normal(sqrt_rn_normal(l2));
   if constexpr (STATS) *flops += 5;
   x = x * il;
   y = y * il;
@@ -921,8 +908,18 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS)) void trace_kernel(
     // ---- one ray-color level: hit-anything over all bodies ----
     --rem;
     ++segs;
-    const float len = sqrt_rn(fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
-    const float il = 1.0f / len;                              // vec3a/unit as d * (1/|d|)
+    // |d| and 1/|d| (vec3a/unit as d * (1/|d|)), both correctly rounded; one
+    // range test for the pair: a finite |d|^2 >= 2^-96 puts |d| in
+    // [2^-48, 2^64), inside rcp_rn_normal's range
+    const float len2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    float len, il;
+    if (__builtin_expect(len2 >= 0x1p-96f && len2 <= 0x1.fffffep127f, 1)) {
+      len = sqrt_rn_normal(len2);
+      il = rcp_rn_normal(len);
+    } else {
+      len = sqrt_rn(len2);
+      il = rcp_rn(len);
+    }
     float ux = dx * il, uy = dy * il, uz = dz * il;
     const float tmin = 1e-3f * len;                           // t-min 1e-3 in |d| units (:48)
     if constexpr (STATS) st_fl += 11;                         // |d|, 1/|d|, u, t-min
