@@ -6,7 +6,7 @@
 // rcp_rn_normal) over 2^-126 <= b < 2^126, candidate 4 (rcp_rn, guard
 // included) over all 2^32 bit patterns; sqrt_rn over all 2^32 and
 // sqrt_rn_normal over 2^-96 <= x <= +inf.
-//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/bin/fp_rn_exhaustive tools/fp_rn_exhaustive.hip
+//   built by raytracing-clj_amd/Makefile as lib/fp_rn_exhaustive; tests/test_gpu_fp_rn.py runs it
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
