@@ -192,10 +192,13 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //      default where spp <= 255, albedos lie in [-1, 1], the tree has <= 256
 //      nodes and the frame is at most 65536 pixels wide and high
 //   16 the same walk in the full image (u16 stack of node addresses, u64 sums)
-//   18 BVH in LDS, 8-body leaves (large scenes: C4)
+//   24 22's compact image in 8-wave workgroups (one tree image per 8 waves):
+//      the default for scenes whose 4-body image is too big for 22 (C4),
+//      where it fits three workgroups per CU and 22 applies
+//   18 BVH in LDS, 8-body leaves (large scenes where 24 does not fit)
 //   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
 //    5 linear scan, grouped, table through the scalar cache: a tree too deep
-//    0 = default (22 where it applies, else 16; 18 when the 4-body tree's LDS image is large)
+//    0 = default (22 where it applies, else 16; 24, else 18, when the 4-body tree's LDS image is large)
 // The diagnostic library (lib/librtclj_diag.so) adds, from trace_diag.hip, the
 // A/B variants -- 1, 2 simple scan (LDS, scalar cache), 4 grouped scan in LDS
 // (north_star's LDS-staged scan), 8, 9 packed pairs, 11 BVH with 2-body leaves
@@ -213,6 +216,9 @@ static const Variant& variant_table(int v) {
   // (8-wave workgroups: one tree image for twice the waves)
   static const Variant v18{RT_KW(SRC_LDS, SCAN_BVHO, false, 8), true, false, SCAN_BVHO, 512};
   static const Variant v22{RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7};
+  // (22's image in 8-wave workgroups: one tree image per 8 waves, for trees
+  // too big for 22's 4-wave workgroups)
+  static const Variant v24{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 8), true, false, SCAN_BVHQ7, 512};
   switch (v) {
     case 0: return placeholder;
     case 5: return v5;
@@ -220,6 +226,7 @@ static const Variant& variant_table(int v) {
     case 16: return v16;
     case 18: return v18;
     case 22: return v22;
+    case 24: return v24;
   }
 #ifdef RTCLJ_DIAG
   if (const Variant* d = diag_variant(v)) return *d;
@@ -574,14 +581,17 @@ static size_t lds_of(const DTree& t, int tree, int threads = 256) {
 // variant 22 (the compact image): u8 node indices, depth rows (the dead
 // far-child write goes one above the top, as in 16)
 static int stack_entries_compact(const DTree& t) { return std::max(t.depth, 1); }
-static size_t lds_of_compact(const DTree& t) {
-  return static_cast<size_t>(t.blob_f4) * 16 + static_cast<size_t>(stack_entries_compact(t)) * 256;
+static size_t lds_of_compact(const DTree& t, int threads) {
+  return static_cast<size_t>(t.blob_f4) * 16 + static_cast<size_t>(stack_entries_compact(t)) * threads;
 }
 // LDS a CU can give each of 5 workgroups (160 KB / 5), less the 4-body-leaf
 // kernel's static LDS (pool counter, the 64 pixels' colour sums and pixel
 // table).  (Its registers allow 6; C1's 24.0 KB image fits 6 as well.)
 constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal: no table, 1 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
+// (variant 24's static LDS, 1.4 KB: the 64 pixels' u32 sums and keys, the
+// wrap counts, 8 waves' compaction counters; 2 KB allowed for)
+constexpr size_t kStaticLds8 = 2048;
 
 // selector -> the variant a launch on ds runs
 static int resolve_variant(const rt_dscene& ds, int vsel) {
@@ -607,7 +617,7 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
     if (vsel != 12 && lds_of(t, variant_tree(vsel)) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
     if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
   }
-  if (vsel == 22 && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
+  if ((vsel == 22 || vsel == 24) && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
   return vsel;
 }
 
@@ -628,6 +638,14 @@ static int launch_variant(const rt_dscene& ds, const rt_params& p) {
   const int sel = g_variant.load();
   int vsel = resolve_variant(ds, sel);
   if ((sel == 0 && vsel == 16) || vsel == 22) vsel = compact_ok(ds, p) ? 22 : 16;
+  // A scene the default sends to the 8-body-leaf walk (its 4-body image too
+  // big for five 4-wave workgroups a CU) runs 22's compact image in 8-wave
+  // workgroups instead where three of those fit a CU: the same 6 waves per
+  // SIMD as 18 (75 VGPRs), on the 4-body walk's leaf records.  C4: 4.592 vs
+  // 4.931 s, same box (profiles/r05/c4_v24/).
+  if (sel == 0 && vsel == 18 && compact_ok(ds, p) && lds_of_compact(ds.tree[1], 512) + kStaticLds8 <= 160 * 1024 / 3)
+    vsel = 24;
+  if (vsel == 24 && !compact_ok(ds, p)) vsel = 16;
   return vsel;
 }
 
@@ -637,7 +655,7 @@ extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_var
 static size_t launch_lds(const rt_dscene& ds, int vsel) {
   const Variant& v = variant_table(vsel);
   if (v.scan == SCAN_BVHS) return static_cast<size_t>(ds.tree[1].blob_f4) * 16 + kXBytes;   // blob | exchange
-  if (vsel == 22) return lds_of_compact(ds.tree[1]);
+  if (vsel == 22 || vsel == 24) return lds_of_compact(ds.tree[1], v.threads);
   if (vsel >= 11) {
     const DTree& tr = ds.tree[variant_tree(vsel)];
     return v.lds ? lds_of(tr, variant_tree(vsel), v.threads) : stack_of(tr, variant_tree(vsel), v.threads);
@@ -806,7 +824,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // entries per lane: the ordered traversal (trees 1, 2) holds at most depth
   // (a node on level L has L - 1 ancestors; the dead far-child write goes one
   // above them); tree 0 also serves the while-while variants (depth + 2)
-  a.bvh_stack = vsel == 22 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
+  a.bvh_stack = vsel == 22 || vsel == 24 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   // drain compaction: a post holds as many paths as a wave's stack slice has

@@ -73,17 +73,20 @@ def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
             assert np.array_equal(got, want), (w, h, spp, depth, k)
 
 
-def test_compaction_on_the_eight_body_leaf_traversal(gpu_lib, monkeypatch):
-    """C4's 1000-body scene runs the 8-body-leaf tree with a u8 stack (half
-    the room per post): a strip at depth 64 equals the mirror with
-    compaction on (the default) and at threshold 3."""
+@pytest.mark.parametrize("v", [18, 24])
+def test_compaction_on_the_eight_wave_traversals(gpu_lib, monkeypatch, v):
+    """C4's 1000-body scene in 8-wave workgroups -- the 8-body-leaf tree with
+    a u8 stack (half the room per post; the scene's resolved variant) and the
+    4-body compact image (24, its default launch): a strip at depth 64 equals
+    the mirror with compaction on (the default) and at threshold 3."""
     from rtclj import scenes
     from rtclj._lib import check, lib
     sc = scenes.cover_c4()
     ds = C.c_void_p()
     check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+    old = lib.rt_set_variant(v)
     try:
-        assert lib.rt_resolve_variant(ds) == 18
+        assert old >= 0
         w, h, spp, depth = 64, 16, 12, 64
         cam = scenes.cover_camera(w, h)
         want = _mirror(sc, cam, w, h, spp, depth, 4)
@@ -93,4 +96,5 @@ def test_compaction_on_the_eight_body_leaf_traversal(gpu_lib, monkeypatch):
             got = _frame(gpu_lib, ds, cam, w, h, spp, depth, 4)
             assert np.array_equal(got, want), thr
     finally:
+        lib.rt_set_variant(old)
         lib.rt_scene_free(ds)

@@ -33,6 +33,9 @@ def main():
          dict(spp=24, n_devices=8, flags=RT_FLAG_SHARDS_ON_DEVICE0)),
         ("realm", ref, R.camera(200, 112, **R.REFERENCE_CAMERA), 200, 112, dict(spp=8, flags=RT_FLAG_REALM)),
         ("spp 300", cover, scenes.cover_camera(96, 54), 96, 54, dict(spp=300)),
+        ("c4 scene", scenes.cover_c4(), scenes.cover_camera(320, 180), 320, 180, dict(spp=40, max_depth=64)),
+        ("c4 scene rows", scenes.cover_c4(), scenes.cover_camera(7680, 4320), 7680, 4320,
+         dict(spp=4, max_depth=64, rows=(2000, 2040))),
     ]
     bad = 0
     for name, sc, cam, w, h, kw in cases:
