@@ -340,7 +340,7 @@ def occupancy(ds, p):
     check(lib.rt_launch_occupancy(ds, C.byref(p), o))
     # o[0]: resident workgroups per CU in 256-thread units (4 waves each; the
     # 8-body-leaf variants run 512-thread workgroups: half as many, 8 waves)
-    threads = 512 if o[3] in (18, 19, 24) else 256
+    threads = {18: 512, 19: 512, 24: 512, 26: 1024}.get(o[3], 256)
     return {"limit_waves_per_simd": min(8.0, o[0] * 4 / 4.0), "workgroups_per_cu": o[0] * 256 // threads,
             "threads_per_workgroup": threads, "vgprs": o[1],
             "lds_bytes_per_wg": o[2], "variant": o[3], "hw_max_waves_per_simd": 8}

@@ -289,8 +289,8 @@ int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_s
 /* Kernel variant selector (all variants give identical bits).  The product
  * library holds: 0 = default (22 where it applies, else 16; when the 4-body
  * tree's LDS image would cap a CU below 5 workgroups and the 8-body tree's
- * is smaller: 24 where 22 applies and three of its 8-wave workgroups fit a
- * CU, else 18);
+ * is smaller: 26 where 22 applies and two of its 16-wave workgroups fit a
+ * CU, else 24 where three of its 8-wave workgroups fit, else 18);
  * 16 = BVH traversal, 4 bodies per leaf, nodes and leaf bodies in LDS;
  * 18 = the same with 8 bodies per leaf, in 512-thread workgroups (one LDS
  * image per 8 waves); 22 = 16 in a compact LDS image (u8 node-index stack,
@@ -298,7 +298,7 @@ int rt_quantize_device(const float* d_lin, uint8_t* d_out, size_t n, void* hip_s
  * CU; 0 selects it wherever spp < 65536, every albedo lies in [-1, 1], the
  * tree has <= 256 nodes and no frame side exceeds 65536, else 16); 24 = 22's
  * image in 512-thread workgroups (one per 8 waves; 16 where 22 does not
- * apply); 12 = BVH
+ * apply); 26 = the same in 1024-thread workgroups (8 waves per SIMD); 12 = BVH
  * with 2 bodies per leaf read from global memory (the fallback for a tree
  * too big for LDS); 5 = linear scan, bodies in groups of 4 through the
  * scalar cache (the fallback for a tree too deep for the stack).  The
@@ -316,7 +316,7 @@ int rt_set_variant(int variant);
 
 /* The kernel variant the current selector resolves to for ds (the default
  * resolved for this scene, or a fallback when a tree does not fit), before
- * the per-launch choice of the compact image (16 -> 22, 18 -> 24), which also
+ * the per-launch choice of the compact image (16 -> 22, 18 -> 26 / 24), which also
  * depends on the launch (spp < 65536, frame size): rt_launch_occupancy's
  * out4[3] reports the variant a given launch runs.  For reading the matching
  * statistics build.  -1 on a NULL scene. */

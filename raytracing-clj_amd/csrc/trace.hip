@@ -192,13 +192,14 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //      default where spp <= 255, albedos lie in [-1, 1], the tree has <= 256
 //      nodes and the frame is at most 65536 pixels wide and high
 //   16 the same walk in the full image (u16 stack of node addresses, u64 sums)
-//   24 22's compact image in 8-wave workgroups (one tree image per 8 waves):
-//      the default for scenes whose 4-body image is too big for 22 (C4),
-//      where it fits three workgroups per CU and 22 applies
+//   26 22's compact image in 16-wave workgroups (one tree image per 16
+//      waves, 64 VGPRs: 8 waves per SIMD): the default for scenes whose
+//      4-body image is too big for 22 (C4), where 22 applies and two fit a CU
+//   24 the same in 8-wave workgroups: where three of those fit and not two of 26's
 //   18 BVH in LDS, 8-body leaves (large scenes where 24 does not fit)
 //   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
 //    5 linear scan, grouped, table through the scalar cache: a tree too deep
-//    0 = default (22 where it applies, else 16; 24, else 18, when the 4-body tree's LDS image is large)
+//    0 = default (22 where it applies, else 16; 26, 24, else 18, when the 4-body tree's LDS image is large)
 // The diagnostic library (lib/librtclj_diag.so) adds, from trace_diag.hip, the
 // A/B variants -- 1, 2 simple scan (LDS, scalar cache), 4 grouped scan in LDS
 // (north_star's LDS-staged scan), 8, 9 packed pairs, 11 BVH with 2-body leaves
@@ -219,6 +220,8 @@ static const Variant& variant_table(int v) {
   // (22's image in 8-wave workgroups: one tree image per 8 waves, for trees
   // too big for 22's 4-wave workgroups)
   static const Variant v24{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 8), true, false, SCAN_BVHQ7, 512};
+  // (and in 16-wave workgroups, 64 VGPRs: 8 waves per SIMD)
+  static const Variant v26{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 16), true, false, SCAN_BVHQ7, 1024};
   switch (v) {
     case 0: return placeholder;
     case 5: return v5;
@@ -227,6 +230,7 @@ static const Variant& variant_table(int v) {
     case 18: return v18;
     case 22: return v22;
     case 24: return v24;
+    case 26: return v26;
   }
 #ifdef RTCLJ_DIAG
   if (const Variant* d = diag_variant(v)) return *d;
@@ -589,8 +593,8 @@ static size_t lds_of_compact(const DTree& t, int threads) {
 // table).  (Its registers allow 6; C1's 24.0 KB image fits 6 as well.)
 constexpr size_t kStaticLds = 4 + kPoolPx * 3 * 8 + kPoolPx * 16 + 12;   // (the 8-body traversal: no table, 1 KB less)
 constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
-// (variant 24's static LDS, 1.4 KB: the 64 pixels' u32 sums and keys, the
-// wrap counts, 8 waves' compaction counters; 2 KB allowed for)
+// (variants 24 / 26's static LDS, 1.4 / 1.5 KB: the 64 pixels' u32 sums and
+// keys, the wrap counts, 8 or 16 waves' compaction counters; 2 KB allowed for)
 constexpr size_t kStaticLds8 = 2048;
 
 // selector -> the variant a launch on ds runs
@@ -617,7 +621,7 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
     if (vsel != 12 && lds_of(t, variant_tree(vsel)) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
     if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
   }
-  if ((vsel == 22 || vsel == 24) && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
+  if ((vsel == 22 || vsel == 24 || vsel == 26) && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
   return vsel;
 }
 
@@ -639,13 +643,20 @@ static int launch_variant(const rt_dscene& ds, const rt_params& p) {
   int vsel = resolve_variant(ds, sel);
   if ((sel == 0 && vsel == 16) || vsel == 22) vsel = compact_ok(ds, p) ? 22 : 16;
   // A scene the default sends to the 8-body-leaf walk (its 4-body image too
-  // big for five 4-wave workgroups a CU) runs 22's compact image in 8-wave
-  // workgroups instead where three of those fit a CU: the same 6 waves per
-  // SIMD as 18 (75 VGPRs), on the 4-body walk's leaf records.  C4: 4.592 vs
-  // 4.931 s, same box (profiles/r05/c4_v24/).
-  if (sel == 0 && vsel == 18 && compact_ok(ds, p) && lds_of_compact(ds.tree[1], 512) + kStaticLds8 <= 160 * 1024 / 3)
-    vsel = 24;
-  if (vsel == 24 && !compact_ok(ds, p)) vsel = 16;
+  // big for five 4-wave workgroups a CU) runs 22's compact image on the
+  // 4-body walk's leaf records instead, in workgroups that share one image
+  // among more waves: 16-wave workgroups (26) where two fit a CU -- 8 waves
+  // per SIMD in 64 VGPRs -- else 8-wave ones (24) where three fit -- 6 per
+  // SIMD, as 18.  C4: 4.295 s (26) vs 4.570 (24) vs 4.931 (18), same boxes
+  // (profiles/r05/c4_v26/, c4_v24/); C2's frame on 26 instead of 22: 260.4 vs
+  // 251.8 ms (a pool's 32,000 samples over 1,024 lanes drain too often).
+  if (sel == 0 && vsel == 18 && compact_ok(ds, p)) {
+    if (lds_of_compact(ds.tree[1], 1024) + kStaticLds8 <= 160 * 1024 / 2)
+      vsel = 26;
+    else if (lds_of_compact(ds.tree[1], 512) + kStaticLds8 <= 160 * 1024 / 3)
+      vsel = 24;
+  }
+  if ((vsel == 24 || vsel == 26) && !compact_ok(ds, p)) vsel = 16;
   return vsel;
 }
 
@@ -655,7 +666,7 @@ extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_var
 static size_t launch_lds(const rt_dscene& ds, int vsel) {
   const Variant& v = variant_table(vsel);
   if (v.scan == SCAN_BVHS) return static_cast<size_t>(ds.tree[1].blob_f4) * 16 + kXBytes;   // blob | exchange
-  if (vsel == 22 || vsel == 24) return lds_of_compact(ds.tree[1], v.threads);
+  if (vsel == 22 || vsel == 24 || vsel == 26) return lds_of_compact(ds.tree[1], v.threads);
   if (vsel >= 11) {
     const DTree& tr = ds.tree[variant_tree(vsel)];
     return v.lds ? lds_of(tr, variant_tree(vsel), v.threads) : stack_of(tr, variant_tree(vsel), v.threads);
@@ -824,7 +835,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // entries per lane: the ordered traversal (trees 1, 2) holds at most depth
   // (a node on level L has L - 1 ancestors; the dead far-child write goes one
   // above them); tree 0 also serves the while-while variants (depth + 2)
-  a.bvh_stack = vsel == 22 || vsel == 24 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
+  a.bvh_stack = vsel == 22 || vsel == 24 || vsel == 26 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   // drain compaction: a post holds as many paths as a wave's stack slice has

@@ -358,14 +358,16 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHS ? 16 : kTile; }
 // (C4: 8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).
 // Without the bound the unit loop's longer-lived uniform values (SGPRs at
 // their limit, copied into VGPRs) take it to ~100 VGPRs and four waves; with
-// it, a few of them spill to scratch outside the hot loop.  HIP passes
+// it, a few of them spill to scratch outside the hot loop.  The compact
+// image's 16-wave workgroups (variant 26) ask for 8: 64 VGPRs, 16 bytes of
+// scratch.  HIP passes
 // __launch_bounds__'s second argument on as amdgpu_waves_per_eu: a count of
 // waves per SIMD, whatever the workgroup's size.  The 8-body-leaf kernel asks
 // for 3 (a register budget of 168): it allocates 75 VGPRs either way, and
 // the schedule made under 3 is C4's faster one -- 4.996 vs 5.019 s with 6
 // asked, same box (profiles/r05/launch_bound/).
-constexpr int min_waves(int scan, bool stats) {
-  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? 7 : scan == SCAN_BVHO ? 3 : 1;
+constexpr int min_waves(int scan, bool stats, int nw = 4) {
+  return stats ? 1 : scan == SCAN_BVHQ ? 6 : scan == SCAN_BVHQ7 ? (nw == 16 ? 8 : 7) : scan == SCAN_BVHO ? 3 : 1;
 }
 
 // The diagnostic scans (SCAN_SIMPLE, SCAN_PK4: the linear scans of the A/B
@@ -375,11 +377,11 @@ template <int SRC, int SCAN, class F>
 __device__ void diag_scan(const struct KArgs& a, const float4* s_geo, float ox, float oy, float oz, float ux,
                           float uy, float uz, F&& consider);
 
-// NW waves per workgroup (4; 8 for the 8-body-leaf walk, whose large LDS
-// image one workgroup of 8 waves shares: 3 workgroups = 6 waves per SIMD on
-// C4's 1000-body tree, where 4-wave workgroups fit 5 per CU = 5 waves)
+// NW waves per workgroup (4; 8 or 16 for trees whose large LDS image more
+// waves share: C4's 1000-body tree as the compact 4-body image, two 16-wave
+// workgroups = 8 waves per SIMD, where 4-wave workgroups fit 3 per CU)
 template <int SRC, int SCAN, bool STATS = false, int NW = 4>
-__global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS)) void trace_kernel(const KArgs a) {
+__global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_kernel(const KArgs a) {
   constexpr int NT = 64 * NW;   // threads
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
   // indices j in [0, npx * spp), sample-major (j -> pixel j % npx, sample
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS)) void trace_kernel(
     const int M = ka->n_owner;
     const int w0 = static_cast<int>(mix32(static_cast<uint32_t>(unit)) % static_cast<uint32_t>(M));
     unsigned long long key = 0;
-    for (int i = 0; i < 512 / NT; ++i) {
+    for (int i = 0; i < (512 + NT - 1) / NT; ++i) {
       int w = w0 + static_cast<int>(threadIdx.x) + NT * i;
       w = w >= M ? w - M : w;
       w = w >= M ? w % M : w;

@@ -144,7 +144,7 @@ def test_version_and_variant():
     from rtclj._lib import diag_lib
     assert b"gfx950" in rtclj.lib.rt_version()
     # the product build holds the default traversal and its fallbacks only
-    for v in (5, 12, 16, 18, 22, 24):
+    for v in (5, 12, 16, 18, 22, 24, 26):
         old = rtclj.lib.rt_set_variant(v)
         assert rtclj.lib.rt_set_variant(old) == v
     for v in (2, 3, 11, 17, 99, -1):
@@ -153,11 +153,11 @@ def test_version_and_variant():
     # the diagnostic build (trace_diag.hip) holds every variant but the
     # dropped while-while traversal (14, 15)
     d = diag_lib()
-    for v in [v for v in range(1, 25) if v not in (14, 15, 23)]:
+    for v in [v for v in range(1, 27) if v not in (14, 15, 23, 25)]:
         assert d.rt_set_variant(v) >= 0, v
-    for v in (14, 15, 23):
+    for v in (14, 15, 23, 25):
         assert d.rt_set_variant(v) == -1 and b"not in this build" in d.rt_last_error()
-    assert d.rt_set_variant(0) == 24
+    assert d.rt_set_variant(0) == 26
     assert rtclj.lib.rt_resolve_variant(None) == -1
     out4 = (C.c_int * 4)()
     assert rtclj.lib.rt_launch_occupancy(None, None, out4) < 0   # NULL scene: error, no device call

@@ -73,12 +73,13 @@ def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
             assert np.array_equal(got, want), (w, h, spp, depth, k)
 
 
-@pytest.mark.parametrize("v", [18, 24])
+@pytest.mark.parametrize("v", [18, 24, 26])
 def test_compaction_on_the_eight_wave_traversals(gpu_lib, monkeypatch, v):
-    """C4's 1000-body scene in 8-wave workgroups -- the 8-body-leaf tree with
-    a u8 stack (half the room per post; the scene's resolved variant) and the
-    4-body compact image (24, its default launch): a strip at depth 64 equals
-    the mirror with compaction on (the default) and at threshold 3."""
+    """C4's 1000-body scene in 8- and 16-wave workgroups -- the 8-body-leaf
+    tree with a u8 stack (half the room per post; the scene's resolved
+    variant) and the 4-body compact image (24; 26, its default launch): a
+    strip at depth 64 equals the mirror with compaction on (the default) and
+    at threshold 3."""
     from rtclj import scenes
     from rtclj._lib import check, lib
     sc = scenes.cover_c4()

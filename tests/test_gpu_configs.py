@@ -203,13 +203,13 @@ def test_c4_against_fp64_reference_semantics(gpu_lib):
     check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
     try:
         # the scene resolves to the 8-body-leaf tree; its launches run the
-        # 4-body compact image in 8-wave workgroups (variant 24), three per CU
+        # 4-body compact image in 16-wave workgroups (variant 26), two per CU
         assert lib.rt_resolve_variant(ds) == 18
         from rtclj._lib import rt_params
         p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=2000, max_depth=depth, seed=1)
         o = (C.c_int * 4)()
         check(lib.rt_launch_occupancy(ds, C.byref(p), o))
-        assert o[3] == 24 and o[0] * 256 // 512 == 3, list(o)
+        assert o[3] == 26 and o[0] * 256 // 1024 == 2, list(o)
     finally:
         lib.rt_scene_free(ds)
     rows, segs32, smp32 = _launch_rows(sc, cam, w, h, spp, depth, row_tile=1, tile_first=0, tile_step=270)

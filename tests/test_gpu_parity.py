@@ -18,7 +18,7 @@ TOL_ABS = 1e-4
 TOL_FRAC = 0.995
 
 
-PRODUCT_VARIANTS = (0, 5, 12, 16, 18, 22, 24)
+PRODUCT_VARIANTS = (0, 5, 12, 16, 18, 22, 24, 26)
 
 
 class variant:
@@ -183,7 +183,7 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("v", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 19, 22, 24])
+@pytest.mark.parametrize("v", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 19, 22, 24, 26])
 def test_every_variant_is_bit_exact(gpu_lib, v):
     """Kernel variants (product and diagnostic builds: table in LDS / scalar
     cache, simple / grouped / packed scan, BVH traversals, stats builds) all
@@ -297,7 +297,7 @@ def test_c1_frame_properties(gpu_lib):
     _assert_parity(a[300:302], ref, "C1 rows 300-301")
 
 
-@pytest.mark.parametrize("v", [11, 12, 16, 18, 22, 24])
+@pytest.mark.parametrize("v", [11, 12, 16, 18, 22, 24, 26])
 def test_bvh_bit_exact_on_full_c1_and_reference(gpu_lib, v):
     """The BVH traversal returns the scan's hits bit for bit: full C1 frame
     (1200x675, 100 spp) and the reference scene, BVH vs brute-force scan."""
@@ -352,10 +352,10 @@ def test_bvh_small_scenes(gpu_lib, n):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
     out = {}
-    for v in (5, 11, 16, 18, 22, 24):
+    for v in (5, 11, 16, 18, 22, 24, 26):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 48, 27, spp=8, max_depth=20, seed=5, library=dll)
-    for v in (11, 16, 18, 22, 24):
+    for v in (11, 16, 18, 22, 24, 26):
         assert np.array_equal(out[5], out[v]), v
     ref, _, _ = _mirror(sc, cam, 48, 27, 8, 20, seed=5)
     assert np.array_equal(out[5], ref)
@@ -384,10 +384,10 @@ def test_bvh_big_bodies(gpu_lib, n_big):
     sc = R.Scene(sph, kind, mat)
     cam = R.camera(64, 36, **R.REFERENCE_CAMERA)
     out = {}
-    for v in (5, 11, 16, 18, 22, 24):
+    for v in (5, 11, 16, 18, 22, 24, 26):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 64, 36, spp=8, max_depth=20, seed=9, library=dll)
-    for v in (11, 16, 18, 22, 24):
+    for v in (11, 16, 18, 22, 24, 26):
         assert np.array_equal(out[5], out[v]), v
     ref, _, _ = _mirror(sc, cam, 64, 36, 8, 20, seed=9)
     assert np.array_equal(out[5], ref)
@@ -396,8 +396,9 @@ def test_bvh_big_bodies(gpu_lib, n_big):
 def test_bvh_cover16_u8_stack_and_u16_indices(gpu_lib):
     """C4's scene (cover grid 16, 1025 bodies): the 8-body-leaf traversal
     (u8 stack, u16 body indices, leaves in two halves; the scene's resolved
-    variant), the 4-body one, and the 4-body compact image in 4- and 8-wave
-    workgroups (22, 24: the default launch here) == the scan == the mirror."""
+    variant), the 4-body one, and the 4-body compact image in 4-, 8- and
+    16-wave workgroups (22, 24, 26: the default launch here) == the scan ==
+    the mirror."""
     import ctypes as C
     from rtclj import raytracing as R
     from rtclj import scenes
@@ -411,10 +412,10 @@ def test_bvh_cover16_u8_stack_and_u16_indices(gpu_lib):
     finally:
         lib.rt_scene_free(ds)
     out = {}
-    for v in (0, 5, 16, 18, 22, 24):
+    for v in (0, 5, 16, 18, 22, 24, 26):
         with variant(v) as dll:
             out[v] = R.render(sc, cam, 96, 54, spp=6, max_depth=64, seed=4, library=dll)
-    for v in (0, 16, 18, 22, 24):
+    for v in (0, 16, 18, 22, 24, 26):
         assert np.array_equal(out[5], out[v]), v
     ref, _, _ = _mirror(sc, cam, 96, 54, 6, 64, seed=4)
     assert np.array_equal(out[5], ref)
@@ -453,7 +454,7 @@ def test_bvh_8body_tree_over_256_nodes_uses_4body(gpu_lib):
     assert np.array_equal(out[5], out[18])
 
 
-@pytest.mark.parametrize("vsel", [0, 11, 16, 18, 22, 24])
+@pytest.mark.parametrize("vsel", [0, 11, 16, 18, 22, 24, 26])
 def test_bvh_large_scene_falls_back(gpu_lib, vsel):
     """8192 bodies: the trees exceed the LDS budget, the launch falls back to
     the global-memory traversal of the 2-body tree: same bits as the scan."""
@@ -484,7 +485,7 @@ def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
     return out, segs, smp
 
 
-@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18, 22, 24])
+@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18, 22, 24, 26])
 def test_realm_flag_matches_mirror(gpu_lib, vsel):
     """RT_FLAG_REALM (realm.raytracing semantics) through the kernel == the
     oracle's MODE_REALM32, bit for bit: the realm scene and the cover scene."""

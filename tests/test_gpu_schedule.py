@@ -51,7 +51,7 @@ def _render(sc, cam, w, h, spp, **kw):
     return R.render(sc, cam, w, h, spp=spp, max_depth=50, **kw)
 
 
-@pytest.mark.parametrize("v", [0, 5, 12, 16, 18, 11, 22, 24])
+@pytest.mark.parametrize("v", [0, 5, 12, 16, 18, 11, 22, 24, 26])
 def test_repeated_launches_are_bit_identical(env, v):
     from rtclj import scenes
     from rtclj._lib import diag_lib, lib
@@ -59,7 +59,7 @@ def test_repeated_launches_are_bit_identical(env, v):
     w, h, spp = 333, 187, 6                       # ragged tiles at both edges
     cam = scenes.cover_camera(w, h)
     want = _render(sc, cam, w, h, spp)
-    dll = lib if v in (0, 5, 12, 16, 18, 24) else diag_lib()
+    dll = lib if v in (0, 5, 12, 16, 18, 24, 26) else diag_lib()
     ds = env[1]
     if dll is not lib:                            # the diagnostic build's own device scene
         ds = C.c_void_p()
