@@ -207,6 +207,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 // statistics builds 3, 6, 7, 10, 13, 17 (= 16 + stats), 19 (= 18 + stats).
 // Every variant renders the same bits.
 // the tree a traversal variant walks: 0 = 2-body leaves, 1 = 4, 2 = 8
+const void* trace_kernel_w16();   // trace_w16.hip
 static int variant_tree(int v) { return v >= 20 ? 1 : v >= 18 ? 2 : v >= 16 ? 1 : 0; }
 static const Variant& variant_table(int v) {
   static const Variant none{nullptr, false, false, 0};
@@ -221,7 +222,8 @@ static const Variant& variant_table(int v) {
   // too big for 22's 4-wave workgroups)
   static const Variant v24{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 8), true, false, SCAN_BVHQ7, 512};
   // (and in 16-wave workgroups, 64 VGPRs: 8 waves per SIMD)
-  static const Variant v26{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 16), true, false, SCAN_BVHQ7, 1024};
+  // (trace_w16.hip, compiled with its own scheduler flag)
+  static const Variant v26{trace_kernel_w16(), true, false, SCAN_BVHQ7, 1024};
   switch (v) {
     case 0: return placeholder;
     case 5: return v5;
