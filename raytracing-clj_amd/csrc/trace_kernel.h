@@ -345,7 +345,8 @@ static_assert(sizeof(KNode) == 80, "KNode layout");
 // The pool tile: 8 x 8 pixels.  (The 8-body-leaf traversal ran 8 x 4 tiles
 // while its 256-thread workgroups were LDS-bound at 5 per CU; in 512-thread
 // workgroups, 3 per CU by registers, the 8 x 8 pool's longer workgroup
-// lifetimes are worth 1 %: C4 4.95 vs 4.99 s, profiles/r05/c4_tile/)
+// lifetimes were worth 1 %: C4 4.95 vs 4.99 s, profiles/r05/c4_tile/.  C4
+// now runs the compact 4-body image in 16-wave workgroups, variant 26.)
 constexpr int kTile = 8;
 // the 4-body tree's leaf record in LDS: two pairs and their index pairs
 constexpr int kLeafRecBytes = 80;
@@ -355,12 +356,13 @@ constexpr int tile_rows(int scan) { return scan == SCAN_BVHS ? 16 : kTile; }
 // Waves per SIMD the register allocator must leave room for: seven for the
 // compact image (72 VGPRs; 23.0 KB of LDS fits 7 workgroups per CU), six
 // for the 4-body traversal (80 VGPRs; 26.6 KB) and for the 8-body-leaf one
-// (C4: 8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).
+// (8-wave workgroups, 3 per CU by registers; 34.4 KB of LDS each).
 // Without the bound the unit loop's longer-lived uniform values (SGPRs at
 // their limit, copied into VGPRs) take it to ~100 VGPRs and four waves; with
 // it, a few of them spill to scratch outside the hot loop.  The compact
-// image's 16-wave workgroups (variant 26) ask for 8: 64 VGPRs, 16 bytes of
-// scratch.  HIP passes
+// image's 16-wave workgroups (variant 26, C4) ask for 8: 64 VGPRs and 16
+// bytes of scratch under the default scheduler, 62 and none under the
+// register-pressure trackers it is compiled with (trace_w16.hip).  HIP passes
 // __launch_bounds__'s second argument on as amdgpu_waves_per_eu: a count of
 // waves per SIMD, whatever the workgroup's size.  The 8-body-leaf kernel asks
 // for 3 (a register budget of 168): it allocates 75 VGPRs either way, and
@@ -642,8 +644,8 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   if (threadIdx.x < NPX * 3) s_acc[threadIdx.x] = 0;
   // the tile's pixel table (4-body-leaf traversal): per pool pixel its RNG
   // key and coordinates, so a camera sample costs one LDS read instead of
-  // the index arithmetic and two hashes (the 8-body-leaf traversal's LDS
-  // image has no room for it: C4 keeps 5 workgroups per CU)
+  // the index arithmetic and two hashes (the 8-body-leaf traversal, whose
+  // workgroups are register-bound, computes them instead)
   constexpr bool kPixelTable = is_q(SCAN);
   // (the compact variant: the keys alone, 4 bytes a pixel, and the image row
   // of each of the tile's rows as a float; a pixel's column is q mod vw)
