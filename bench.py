@@ -50,7 +50,8 @@ import torch.distributed as dist  # noqa: E402
 import rtclj  # noqa: E402
 from rtclj import raytracing as R  # noqa: E402
 from rtclj import scenes  # noqa: E402
-from rtclj._lib import RT_FLAG_SHARDS_ON_DEVICE0, RT_FLAG_STREAMED, check, diag_lib, lib, rt_params  # noqa: E402
+from rtclj._lib import RT_FLAG_REJECTION_SAMPLERS, RT_FLAG_SHARDS_ON_DEVICE0, RT_FLAG_STREAMED, check, diag_lib, lib, \
+    rt_params  # noqa: E402
 from rtclj.shard import shard_params, shard_rows  # noqa: E402
 
 # BASELINE.json's metric is quoted on C1; the other workloads report the same
@@ -101,12 +102,17 @@ def parse():
                     help="seconds of back-to-back single-stream frames after the timed steps, reported as "
                          "`sustained` (clocks and power under a long load; default 5 for c1, 0 otherwise)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--samplers", choices=["direct", "rejection"], default="direct",
+                    help="direct (the product default): the loop-free samplers; rejection: vec3a.clj:74-86's "
+                         "rejection loops (RT_FLAG_REJECTION_SAMPLERS) on every launch of the run")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-row-step", type=int, default=2, help="CPU baseline samples rows 0, s, 2s, ...")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--e2e", choices=["auto", "off"], default="auto", help="time rt_render end to end on rank 0")
     ap.add_argument("--stats", choices=["auto", "off"], default="auto", help="one untimed stats-build launch")
     a = ap.parse_args()
+    global SAMPLER_FLAGS
+    SAMPLER_FLAGS = RT_FLAG_REJECTION_SAMPLERS if a.samplers == "rejection" else 0
     if a.steps is None:
         a.steps = 100 if a.workload == "c1" else 5
     if a.warmup is None:
@@ -155,14 +161,20 @@ def cpu_model():
     return "unknown"
 
 
+# rt_params.flags bits every launch of the run carries (--samplers)
+SAMPLER_FLAGS = 0
+
+
 def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads, gpu_rows, gpu_rows_segs):
     """The oracle's fp64 reference-semantics mode (the C++ restatement of the
     Clojure path) on a bounded row sample of the same frame, on host cores;
-    and the parity of the GPU frame's same rows against it (oracle.pin)."""
+    and the parity of the GPU frame's same rows: statistically against that
+    fp64 render (oracle.pin), and bit for bit against the oracle's fp32 mirror
+    of the kernel's contract on four of those rows."""
     sys.path.insert(0, str(ROOT))
     import numpy as np
     import oracle
-    from oracle.pin import BOUNDS, compare, within
+    from oracle.pin import BOUNDS, BOUNDS_INDEPENDENT, compare, within
     usable, affinity, quota = host_cpus()
     nthreads = threads if threads > 0 else usable
     args = (scene.sphere.astype(np.float64), scene.kind, scene.mat.astype(np.float64), cam.as_list(), cam.defocus,
@@ -189,11 +201,29 @@ def cpu_baseline(scene, cam, w, h, spp, depth, seed, row_step, threads, gpu_rows
                                      f"pool-size 2 (raytracing.clj:157)"}}
     parity = None
     if gpu_rows is not None:
+        direct = not (SAMPLER_FLAGS & RT_FLAG_REJECTION_SAMPLERS)
+        # the default loop-free samplers draw other uniforms than the fp64
+        # restatement's rejection loops: independent paths, statistical bounds
+        bounds = BOUNDS_INDEPENDENT if direct else BOUNDS
         st = compare(ref, segs / samples, gpu_rows, gpu_rows_segs / samples, by=max(1, min(9, rows // 8)))
-        ok = within(st)
+        ok = within(st, bounds)
+        # four of the rows against the fp32 mirror of the same contract and samplers: bit for bit
+        mode = oracle.MODE_MIRROR32 | (oracle.DIRECT if direct else 0)
+        pick = sorted({0, rows // 4, rows // 2, (3 * rows) // 4})
+        t2 = time.perf_counter()
+        exact = []
+        for i in pick:
+            y = i * row_step
+            m, _, _, _ = oracle.render(mode, *args, seed=seed, rows=(y, y + 1), nthreads=nthreads)
+            exact.append(bool(np.array_equal(m[0], gpu_rows[i])))
         parity = {"against": "oracle MODE_REF64 (the Clojure path in double), same rows, same seed",
-                  "rows": f"0,{row_step},...", "stats": st, "bounds": BOUNDS, "pass": all(ok.values()),
-                  "checks": ok}
+                  "draws": "independent (the kernel's loop-free samplers vs the reference's rejection loops)"
+                           if direct else "the same (RT_FLAG_REJECTION_SAMPLERS)",
+                  "rows": f"0,{row_step},...", "stats": st, "bounds": bounds, "checks": ok,
+                  "mirror_rows": {"mode": "MODE_MIRROR32" + (" | DIRECT" if direct else ""),
+                                  "rows": [i * row_step for i in pick], "bit_exact": exact,
+                                  "seconds": time.perf_counter() - t2},
+                  "pass": all(ok.values()) and all(exact)}
     return res, parity
 
 
@@ -365,7 +395,7 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
     the float frame."""
     import numpy as np
     visible = lib.rt_device_count()
-    flags = RT_FLAG_SHARDS_ON_DEVICE0 if n_dev > visible else 0
+    flags = (RT_FLAG_SHARDS_ON_DEVICE0 if n_dev > visible else 0) | SAMPLER_FLAGS
     lib.rt_cache_clear()
     first = {}
     t0 = time.perf_counter()
@@ -429,7 +459,7 @@ def end_to_end(scene, cam, W, H, spp, depth, seed, n_dev, reps=7, warm=3):
         return {k: r[k] for k in PARTS}
 
     return {"entry": "rt_render (include/rt.h)", "n_devices": med["n_devices"],
-            "shards_on_device0": bool(flags), "statistic": f"median of {reps} calls",
+            "shards_on_device0": bool(flags & RT_FLAG_SHARDS_ON_DEVICE0), "statistic": f"median of {reps} calls",
             "total_ms": med["total_ms"], "total_ms_min": runs[0]["total_ms"], "total_ms_max": runs[-1]["total_ms"],
             "kernel_ms_max": med["kernel_ms"], "kernel_ms_mean": med["kernel_ms_mean"],
             "imbalance": med["kernel_ms"] / med["kernel_ms_mean"], "d2h_ms": med["d2h_ms"],
@@ -463,9 +493,10 @@ def first_process(wl, spp, depth, seed, n_dev):
         return None
     with tempfile.TemporaryDirectory() as td:
         t0 = time.perf_counter()
+        extra = ["--rejection-samplers"] if SAMPLER_FLAGS & RT_FLAG_REJECTION_SAMPLERS else []
         r = subprocess.run([str(exe), str(spp), str(depth), "--scene", "cover", "--width", str(wl["width"]),
-                            "--seed", str(seed), "--gpus", str(n_dev), "--out", str(Path(td) / "scene.ppm"), "--json"],
-                           capture_output=True, text=True, timeout=300)
+                            "--seed", str(seed), "--gpus", str(n_dev), "--out", str(Path(td) / "scene.ppm"), "--json"]
+                           + extra, capture_output=True, text=True, timeout=300)
         wall = (time.perf_counter() - t0) * 1e3
     if r.returncode != 0:
         return {"error": (r.stdout + r.stderr)[-400:]}
@@ -553,6 +584,7 @@ def main():
     check(lib.rt_scene_upload(device, C.byref(scene.c), C.byref(ds)))
     _resolved[(id(scene), device)] = lib.rt_resolve_variant(ds)
     p = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
+    p.flags |= SAMPLER_FLAGS
     rows = check(lib.rt_rows_out(C.byref(p)))
     assert rows == len(shard_rows(H, p.row_tile or 8, p.tile_first, p.tile_step))
     # frames in flight: frame k on streams[k % nf], each stream its own
@@ -575,6 +607,7 @@ def main():
 
     def params_for(nf):
         q = rt_params(**shard_params(world, rank, W, H, spp, depth, a.seed, a.scaling))
+        q.flags |= SAMPLER_FLAGS
         if nf > 1:
             q.flags |= RT_FLAG_STREAMED
         return q
@@ -756,7 +789,9 @@ def main():
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "bodies": len(scene),
                        "parallelism": ("row-tile 8 x%d (strong)" % world) if a.scaling == "strong"
                        else ("sample-stripe x%d (weak)" % world), "variant": a.variant,
-                       "tile_schedule": "adaptive longest-first" if a.schedule == 0 else "dispatch order"},
+                       "tile_schedule": "adaptive longest-first" if a.schedule == 0 else "dispatch order",
+                       "samplers": "loop-free (default)" if a.samplers == "direct"
+                       else "rejection (RT_FLAG_REJECTION_SAMPLERS)"},
             "roofline": roof,
             "hbm_roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": gbs / PEAK_HBM_GBS, "traffic": traffic["bytes"] if traffic else None,
@@ -808,7 +843,7 @@ def main():
                 # the GPU frame's rows 0, s, 2s, ... and their own segment count
                 # (one untimed launch of just those rows: 1-row tiles, stride s)
                 pr = rt_params(width=W, height=H, row_begin=0, row_end=H, spp=spp, max_depth=depth, seed=a.seed,
-                               row_tile=1, tile_first=0, tile_step=a.cpu_row_step)
+                               row_tile=1, tile_first=0, tile_step=a.cpu_row_step, flags=SAMPLER_FLAGS)
                 nr = check(lib.rt_rows_out(C.byref(pr)))
                 o2 = torch.empty(nr * W * 3, dtype=torch.float32, device=dev)
                 c2 = torch.zeros(2, dtype=torch.int64, device=dev)

@@ -111,7 +111,8 @@ typedef struct rt_params {
   int row_tile;           /* interleaved tile height (rows); 0 -> 8            */
   int tile_first;         /* rt_launch: first tile of this shard               */
   int tile_step;          /* rt_launch: tile stride (0 = contiguous rows)      */
-  int flags;              /* 0, RT_FLAG_REALM, RT_FLAG_SHARDS_ON_DEVICE0 (rt_render),
+  int flags;              /* 0, RT_FLAG_REALM, RT_FLAG_REJECTION_SAMPLERS,
+                             RT_FLAG_SHARDS_ON_DEVICE0 (rt_render),
                              RT_FLAG_STREAMED (rt_launch), ored                 */
 } rt_params;
 
@@ -137,6 +138,19 @@ typedef struct rt_params {
  * Timing only: the bits never depend on it.  (tools/shard_time.py
  * --inflight; bench.py's frames in flight) */
 #define RT_FLAG_STREAMED 4
+
+/* rt_launch / rt_render: draw vec3a/random-unit-vec3 and random-in-unit-disk
+ * by the reference's own rejection loops (vec3a.clj:74-86: three or two
+ * uniforms per trip until the point falls inside the unit ball / disk).
+ * Without the flag (the default) the kernel draws the same distributions
+ * with a fixed number of draws -- uniform on the sphere as z = 2 xi1 - 1,
+ * r = sqrt(1 - z^2), at the angle 2 pi xi2; uniform in the disk as
+ * r = sqrt(xi1) at 2 pi xi2 -- so a wave no longer waits for its slowest
+ * lane's rejection trips (C1 5.23 -> 4.75 ms per frame).
+ * The reference's rand is unseeded, so either choice matches its renders
+ * statistically (tests/test_oracle_pinning.py); each equals its own fp32
+ * mirror in the oracle bit for bit.  Mixed within one frame never. */
+#define RT_FLAG_REJECTION_SAMPLERS 8
 
 /* ---- per-call statistics (device-side counters, host timers) ------------ */
 typedef struct rt_stats {

@@ -16,6 +16,10 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "_build" / "liboracle.so"
 MODE_REF64, MODE_MIRROR32, MODE_BOOK64, MODE_REALM64, MODE_REALM32 = 0, 1, 2, 3, 4
+# ored into MODE_MIRROR32 / MODE_REALM32: the kernel's loop-free samplers
+# (RT_FLAG_DIRECT_SAMPLERS): the unit-sphere draw, the defocus disk, both
+DIRECT_SPHERE, DIRECT_DISK = 0x10, 0x20
+DIRECT = DIRECT_SPHERE | DIRECT_DISK
 
 _dll = None
 
@@ -54,6 +58,9 @@ def _lib():
         d.oracle_dielectric_dir.restype = C.c_int
         d.oracle_dielectric_dir.argtypes = [dp, dp, C.c_int, C.c_double, C.c_double, dp]
         d.oracle_rng_stream.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, fp]
+        d.oracle_sampler_draws.restype = C.c_int
+        d.oracle_sampler_draws.argtypes = [C.c_int, C.c_uint64, C.c_int, fp]
+        d.oracle_turn24.argtypes = [C.c_int, C.POINTER(C.c_uint32), C.c_float, fp]
         _dll = d
     return _dll
 
@@ -159,3 +166,23 @@ def dielectric_dir(d, n, front, eta, xi):
     o, op = _d(np.zeros(3))
     refl = _lib().oracle_dielectric_dir(ap, bp, int(front), eta, xi, op)
     return bool(refl), o.tolist()
+
+
+SAMPLERS = {"sphere_rejection": 0, "sphere_direct": 1, "disk_rejection": 2, "disk_direct": 3}
+
+
+def sampler_draws(which, seed, n):
+    """n consecutive draws of one sampler from the keyed stream (seed, 0, 0):
+    (n, 3) float32 (the disk's z = 0).  which: a SAMPLERS key."""
+    out = np.zeros((n, 3), np.float32)
+    if _lib().oracle_sampler_draws(SAMPLERS[which], seed, n, out.ctypes.data_as(C.POINTER(C.c_float))) != 0:
+        raise ValueError(which)
+    return out
+
+
+def turn24(u, r=1.0):
+    """The kernel's (r cos, r sin) of 2 pi u / 2^24 for 24-bit integers u: (n, 2) float32."""
+    u = np.ascontiguousarray(u, np.uint32).reshape(-1)
+    out = np.zeros((len(u), 2), np.float32)
+    _lib().oracle_turn24(len(u), u.ctypes.data_as(C.POINTER(C.c_uint32)), r, out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out

@@ -39,9 +39,18 @@ def compare(a64, seg_per_sample64, a32, seg_per_sample32, by):
             "block_mean": float(bd.mean()), "block_max": float(bd.max())}
 
 
+# same draws (the fp32 contract with the reference's rejection samplers,
+# RT_FLAG_REJECTION_SAMPLERS / MODE_MIRROR32): the paths agree except where an
+# fp32 decision flips, so per-pixel bounds hold
 BOUNDS = {"seg_rel": 2e-3, "lin_mean": 5e-4, "px8_mean": 0.25, "px8_off_gt1": 0.02, "block_mean": 0.25,
           "block_max": 2.5}
+# independent draws (the kernel's default loop-free samplers draw the same
+# distributions from a different number of uniforms, so every path after the
+# first scatter differs): the bounds SURVEY.md §8c sets for a render against
+# the reference's own unseeded one -- block means (8-bit) mean |d| <= 0.25,
+# max <= 2.5, per-pixel mean |d| <= 3.5 -- and segments/sample within 2e-3
+BOUNDS_INDEPENDENT = {"seg_rel": 2e-3, "px8_mean": 3.5, "block_mean": 0.25, "block_max": 2.5}
 
 
-def within(st):
-    return {k: st[k] <= v for k, v in BOUNDS.items()}
+def within(st, bounds=None):
+    return {k: st[k] <= v for k, v in (BOUNDS if bounds is None else bounds).items()}

@@ -34,6 +34,10 @@
 //     the caller's rt_camera.
 //   MODE_REALM32 (4) — MODE_MIRROR32 with the kernel's RT_FLAG_REALM: the
 //     same three semantic changes, the pixel as total * RN(1/spp).
+//   mode | 0x10, | 0x20 (MODE_MIRROR32 / MODE_REALM32 only) — the kernel's
+//     loop-free samplers (RT_FLAG_DIRECT_SAMPLERS: 0x10 the unit-sphere draw
+//     of lambertian and metal, 0x20 the defocus disk): the same
+//     distributions as vec3a.clj:74-86, a fixed number of draws.
 //
 // The reference's RNG is clojure.core/rand (unseeded java.util.Random,
 // vec3a.clj:71-72), so no bitwise reference image exists.  Both modes draw
@@ -322,9 +326,53 @@ void random_unit32(Rng& s, float& x, float& y, float& z) {
   z = z * il;
 }
 
+// The kernel's loop-free samplers (RT_FLAG_DIRECT_SAMPLERS;
+// raytracing-clj_amd/csrc/trace_kernel.h turn24 / sphere_direct /
+// disk_direct), op for op: the same distributions as vec3a.clj:74-86's
+// rejection loops -- uniform on the unit sphere (z = 2 xi1 - 1, r = sqrt(1 -
+// z^2)) and in the unit disk (r = sqrt(xi1)) -- at the angle 2 pi xi2, whose
+// (cos, sin) come from the 24-bit integer of xi2: the nearest quarter turn q
+// and Taylor polynomials of the rest (|theta| <= pi/4), rotated by q.
+inline uint32_t u24(Rng& r) {
+  r.s ^= r.s << 13;
+  r.s ^= r.s >> 17;
+  r.s ^= r.s << 5;
+  return r.s >> 8;
+}
+void turn24(uint32_t u, float r, float& x, float& y) {
+  const int32_t f = static_cast<int32_t>(u << 10) >> 10;       // low 22 bits, signed
+  const uint32_t q = (u + 0x200000u) >> 22;                    // nearest quarter turn (mod 4)
+  const float th = static_cast<float>(f) * 0x1.921fb6p-22f;    // RN(2 pi / 2^24)
+  const float t2 = th * th;
+  float ps = std::fmaf(t2, 0x1.71de3ap-19f, -0x1.a01a02p-13f);
+  ps = std::fmaf(t2, ps, 0x1.111112p-7f);
+  ps = std::fmaf(t2, ps, -0x1.555556p-3f);
+  const float sn = std::fmaf(th * t2, ps, th);
+  float pc = std::fmaf(t2, 0x1.a01a02p-16f, -0x1.6c16c2p-10f);
+  pc = std::fmaf(t2, pc, 0x1.555556p-5f);
+  pc = std::fmaf(t2, pc, -0.5f);
+  const float cs = std::fmaf(t2, pc, 1.0f);
+  const bool sw = (q & 1u) != 0;
+  const float a = sw ? sn : cs, b = sw ? cs : sn;
+  const float rx = (((q + 1u) & 2u) != 0) ? -r : r;            // x < 0 for q = 1, 2
+  const float ry = ((q & 2u) != 0) ? -r : r;                   // y < 0 for q = 2, 3
+  x = rx * a;
+  y = ry * b;
+}
+void sphere_direct32(Rng& s, float& x, float& y, float& z) {
+  z = 2.0f * s.uf() - 1.0f;
+  const float r = std::sqrt(std::fmaf(-z, z, 1.0f));
+  turn24(u24(s), r, x, y);
+}
+void disk_direct32(Rng& s, float& x, float& y) {
+  const float r = std::sqrt(s.uf());
+  turn24(u24(s), r, x, y);
+}
+enum { DIRECT_SPHERE = 1, DIRECT_DISK = 2 };   // the kernel's RT_SAMPLER_* bits (mode >> 4)
+
 // one sample of the stackless kernel loop; returns colour, adds segments
-void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int px, int gy, uint32_t st,
-              int max_depth, float* col, uint64_t* segs) {
+void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int direct, int px, int gy,
+              uint32_t st, int max_depth, float* col, uint64_t* segs) {
   Rng rng{st};
   const float fx = static_cast<float>(px) + (rng.uf() - 0.5f);
   const float fy = static_cast<float>(gy) + (rng.uf() - 0.5f);
@@ -334,10 +382,14 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int
   float ox, oy, oz;
   if (defocus) {
     float qx, qy;
-    do {
-      qx = 2.0f * rng.uf() - 1.0f;
-      qy = 2.0f * rng.uf() - 1.0f;
-    } while (!(std::fmaf(qy, qy, qx * qx) < 1.0f));
+    if (direct & DIRECT_DISK) {
+      disk_direct32(rng, qx, qy);
+    } else {
+      do {
+        qx = 2.0f * rng.uf() - 1.0f;
+        qy = 2.0f * rng.uf() - 1.0f;
+      } while (!(std::fmaf(qy, qy, qx * qx) < 1.0f));
+    }
     ox = std::fmaf(cam[15], qy, std::fmaf(cam[12], qx, cam[0]));
     oy = std::fmaf(cam[16], qy, std::fmaf(cam[13], qx, cam[1]));
     oz = std::fmaf(cam[17], qy, std::fmaf(cam[14], qx, cam[2]));
@@ -406,7 +458,10 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int
     const int kind = sc.kind[best];
     if (kind == LAMB) {
       float rx, ry, rz;
-      random_unit32(rng, rx, ry, rz);
+      if (direct & DIRECT_SPHERE)
+        sphere_direct32(rng, rx, ry, rz);
+      else
+        random_unit32(rng, rx, ry, rz);
       float qx = rx + nx, qy = ry + ny, qz = rz + nz;
       if (!realm && std::fabs(qx) < 1e-8f && std::fabs(qy) < 1e-8f && std::fabs(qz) < 1e-8f) {
         qx = nx;
@@ -423,7 +478,10 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int
       const float k2 = 2.0f * std::fmaf(dz, nz, std::fmaf(dy, ny, dx * nx));
       const float rx0 = std::fmaf(-nx, k2, dx), ry0 = std::fmaf(-ny, k2, dy), rz0 = std::fmaf(-nz, k2, dz);
       float qx, qy, qz;
-      random_unit32(rng, qx, qy, qz);
+      if (direct & DIRECT_SPHERE)
+        sphere_direct32(rng, qx, qy, qz);
+      else
+        random_unit32(rng, qx, qy, qz);
       const float rx = std::fmaf(m[3], qx, rx0), ry = std::fmaf(m[3], qy, ry0), rz = std::fmaf(m[3], qz, rz0);
       if (!(std::fmaf(rz, nz, std::fmaf(ry, ny, rx * nx)) > 0.0f)) return;  // absorbed
       dx = rx;
@@ -469,6 +527,7 @@ void sample32(const Scene32& sc, const float* cam, bool defocus, bool realm, int
 
 struct Job {
   int mode;
+  int direct;   // the fp32 modes' loop-free samplers (DIRECT_* bits)
   Scene64 s64;
   Scene32 s32;
   double cam64[18];
@@ -530,7 +589,7 @@ void render_row(const Job& J, int ro, int x0, int x1, uint64_t* segs) {
         uint32_t st = mix32(pk + static_cast<uint32_t>(J.sample_begin + k) * 0x9e3779b9u);
         if (st == 0) st = 0x6d2b79f5u;
         float col[3];
-        sample32(J.s32, J.cam32, J.defocus, realm, px, gy, st, J.max_depth, col, segs);
+        sample32(J.s32, J.cam32, J.defocus, realm, J.direct, px, gy, st, J.max_depth, col, segs);
         sr += fix24(col[0]);
         sg += fix24(col[1]);
         sb += fix24(col[2]);
@@ -570,10 +629,16 @@ int oracle_render_cols(int mode, int n, const double* sphere, const int* kind, c
                        uint64_t seed, int nthreads, float* out, double* out64, uint64_t* counters) {
   if (width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_end < row_begin || !out ||
       row_step <= 0 || col_begin < 0 || col_end > width || col_end < col_begin ||
-      (n > 0 && (!sphere || !kind || !mat)) || !cam || mode < MODE_REF64 || mode > MODE_REALM32)
+      (n > 0 && (!sphere || !kind || !mat)) || !cam || (mode & ~0x3f) != 0)
+    return -1;
+  // mode | (DIRECT_* << 4): the fp32 mirrors with the kernel's loop-free samplers
+  const int direct = (mode >> 4) & (DIRECT_SPHERE | DIRECT_DISK);
+  mode &= 0xf;
+  if (mode < MODE_REF64 || mode > MODE_REALM32 || (direct && mode != MODE_MIRROR32 && mode != MODE_REALM32))
     return -1;
   Job J{};
   J.mode = mode;
+  J.direct = direct;
   J.s64 = Scene64{n, sphere, kind, mat};
   J.s32.n = n;
   J.s32.kind = kind;
@@ -760,6 +825,38 @@ void oracle_camera(int w, int h, double vfov, const double* lf, const double* la
 void oracle_rng_stream(uint64_t seed, uint32_t pixel, uint32_t sample, int n, float* out) {
   Rng r{sample_state(seed_key(seed), pixel, sample)};
   for (int i = 0; i < n; ++i) out[i] = r.uf();
+}
+
+// The samplers alone: n draws from one keyed stream (seed, pixel 0, sample
+// 0), consecutive. which: 0 random_unit32 (vec3a.clj:74-79's rejection loop
+// in fp32), 1 sphere_direct32, 2 the disk's rejection loop (vec3a.clj:81-86),
+// 3 disk_direct32.  out: n x 3 floats (the disk's z = 0).
+int oracle_sampler_draws(int which, uint64_t seed, int n, float* out) {
+  if (which < 0 || which > 3 || n < 0 || (n > 0 && !out)) return -1;
+  Rng r{sample_state(seed_key(seed), 0, 0)};
+  for (int i = 0; i < n; ++i) {
+    float x = 0, y = 0, z = 0;
+    switch (which) {
+      case 0: random_unit32(r, x, y, z); break;
+      case 1: sphere_direct32(r, x, y, z); break;
+      case 2:
+        do {
+          x = 2.0f * r.uf() - 1.0f;
+          y = 2.0f * r.uf() - 1.0f;
+        } while (!(std::fmaf(y, y, x * x) < 1.0f));
+        break;
+      default: disk_direct32(r, x, y); break;
+    }
+    out[3 * i] = x;
+    out[3 * i + 1] = y;
+    out[3 * i + 2] = z;
+  }
+  return 0;
+}
+
+// turn24 for given 24-bit integers: out[2i], out[2i+1] = r (cos, sin) of 2 pi u / 2^24
+void oracle_turn24(int n, const uint32_t* u, float r, float* out) {
+  for (int i = 0; i < n; ++i) turn24(u[i] & 0xffffffu, r, out[2 * i], out[2 * i + 1]);
 }
 
 }  // extern "C"

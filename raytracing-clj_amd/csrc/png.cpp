@@ -213,8 +213,12 @@ extern "C" int rt_ppm_to_png(const char* src, const char* dst) {
     skip();
     const size_t b = pos;
     long x = 0;
-    while (pos < tn && t[pos] >= '0' && t[pos] <= '9') x = x * 10 + (t[pos++] - '0');
-    if (pos == b || pos - b > 9 || (pos < tn && !space(t[pos]))) return false;
+    // (a tenth digit ends the parse before it is multiplied in: no overflow)
+    while (pos < tn && t[pos] >= '0' && t[pos] <= '9') {
+      if (pos - b == 9) return false;
+      x = x * 10 + (t[pos++] - '0');
+    }
+    if (pos == b || (pos < tn && !space(t[pos]))) return false;
     *v = x;
     return true;
   };

@@ -710,7 +710,8 @@ int plan_frame(const rt_scene* s, const rt_camera* c, const rt_params* p, void* 
   if (!s || !c || !p || !out_rgb) return set_error(RT_E_ARG, w + ": NULL argument");
   const bool on_dev0 = (p->flags & RT_FLAG_SHARDS_ON_DEVICE0) != 0;
   if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP || p->n_devices < 0 ||
-      (p->flags & ~(RT_FLAG_SHARDS_ON_DEVICE0 | RT_FLAG_REALM)) != 0 || (on_dev0 && p->n_devices == 0))
+      (p->flags & ~(RT_FLAG_SHARDS_ON_DEVICE0 | RT_FLAG_REALM | RT_FLAG_REJECTION_SAMPLERS)) != 0 ||
+      (on_dev0 && p->n_devices == 0))
     return set_error(RT_E_ARG, w + ": bad width/height/spp/flags/n_devices");
   if (p->tile_step != 0 || p->tile_first != 0)
     return set_error(RT_E_ARG, w + ": tile_first/tile_step are per-shard (rt_launch) fields");
@@ -735,7 +736,7 @@ int plan_frame(const rt_scene* s, const rt_camera* c, const rt_params* p, void* 
     Shard& sh = f->shards[d];
     sh.device = on_dev0 ? 0 : d;
     sh.p = *p;
-    sh.p.flags = p->flags & RT_FLAG_REALM;   // semantics travel; the fan-out flag is rt_render's
+    sh.p.flags = p->flags & (RT_FLAG_REALM | RT_FLAG_REJECTION_SAMPLERS);   // semantics travel; the fan-out flag is rt_render's
     sh.p.row_tile = T;
     if (ndev > 1) {
       sh.p.tile_first = d;

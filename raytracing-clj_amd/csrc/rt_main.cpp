@@ -14,7 +14,7 @@
 //
 //   rt_main [spp] [depth] [--scene reference|cover] [--realm] [--width W]
 //           [--seed S] [--gpus N] [--out PATH] [--png PATH] [--no-png] [--json]
-//           [--host-quantize]
+//           [--host-quantize] [--rejection-samplers]
 // Defaults follow the reference: spp 100, depth 50, width 400, 16:9.
 // --json: one more line, a JSON object of where this one-frame process's time
 // went (the device start-up -- the HIP runtime's first rt_device_count, then
@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
   int spp = 100, depth = 50, width = 400, gpus = 0, grid = 11;
   unsigned long long seed = 1;
   std::string scene = "reference", out, png;
-  bool realm = false, json = false, host_quantize = false, no_png = false;
+  bool realm = false, json = false, host_quantize = false, no_png = false, rejection = false;
   int pos = 0;
   const auto t_start = std::chrono::steady_clock::now();
   auto ms_since = [](std::chrono::steady_clock::time_point t) {
@@ -89,6 +89,7 @@ int main(int argc, char** argv) {
     else if (a == "--out") out = val();
     else if (a == "--png") png = val();
     else if (a == "--realm") realm = true;
+    else if (a == "--rejection-samplers") rejection = true;   // RT_FLAG_REJECTION_SAMPLERS
     else if (a == "--json") json = true;
     else if (a == "--no-png") no_png = true;
     else if (a == "--host-quantize") host_quantize = true;
@@ -146,7 +147,7 @@ int main(int argc, char** argv) {
   p.max_depth = depth;
   p.seed = seed;
   p.n_devices = gpus;
-  p.flags = realm ? RT_FLAG_REALM : 0;
+  p.flags = (realm ? RT_FLAG_REALM : 0) | (rejection ? RT_FLAG_REJECTION_SAMPLERS : 0);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t nch = static_cast<size_t>(width) * height * 3;
   std::vector<uint8_t> q(nch);

@@ -188,14 +188,16 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 // Kernel variants (rt_set_variant).  The product library carries the default
 // traversal and its fallbacks:
 //   22 BVH in LDS, 4-body leaves, compact image (u8 node-index stack, u32
-//      pixel sums, 8-byte pixel table): seven workgroups per CU -- the
-//      default where spp <= 255, albedos lie in [-1, 1], the tree has <= 256
-//      nodes and the frame is at most 65536 pixels wide and high
+//      pixel sums with counted wraps, 8-byte pixel table): seven workgroups
+//      per CU -- the default where spp < 65536, albedos lie in [-1, 1], the
+//      tree has <= 256 nodes and the frame is at most 65536 pixels wide and high
 //   16 the same walk in the full image (u16 stack of node addresses, u64 sums)
 //   26 22's compact image in 16-wave workgroups (one tree image per 16
 //      waves, 64 VGPRs: 8 waves per SIMD): the default for scenes whose
 //      4-body image is too big for 22 (C4), where 22 applies and two fit a CU
 //   24 the same in 8-wave workgroups: where three of those fit and not two of 26's
+//   28 22 on 8 x 4-pixel pools: the default for a launch of 22 with fewer 8 x 8
+//      tiles than twice the workgroups the device holds (a multi-GPU shard)
 //   18 BVH in LDS, 8-body leaves (large scenes where 24 does not fit)
 //   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
 //    5 linear scan, grouped, table through the scalar cache: a tree too deep
@@ -224,6 +226,10 @@ static const Variant& variant_table(int v) {
   // (and in 16-wave workgroups, 64 VGPRs: 8 waves per SIMD)
   // (trace_w16.hip, compiled with its own scheduler flag)
   static const Variant v26{trace_kernel_w16(), true, false, SCAN_BVHQ7, 1024};
+  // (22 on 8 x 4-pixel pools: launches of few 8 x 8 tiles -- a shard of a
+  // multi-GPU frame -- run whole pools of half the pixels instead of sample
+  // splits)
+  static const Variant v28{RT_KWT(SRC_LDS, SCAN_BVHQ7, false, 4, 4), true, false, SCAN_BVHQ7, 256, 4};
   switch (v) {
     case 0: return placeholder;
     case 5: return v5;
@@ -233,6 +239,7 @@ static const Variant& variant_table(int v) {
     case 22: return v22;
     case 24: return v24;
     case 26: return v26;
+    case 28: return v28;
   }
 #ifdef RTCLJ_DIAG
   if (const Variant* d = diag_variant(v)) return *d;
@@ -599,14 +606,45 @@ constexpr size_t kLds5 = 160 * 1024 / 5 - kStaticLds;
 // keys, the wrap counts, 8 or 16 waves' compaction counters; 2 KB allowed for)
 constexpr size_t kStaticLds8 = 2048;
 
+// Tile sharing (DESIGN.md §3.1), A/B knobs read at every launch:
+// RTCLJ_STEAL=0 (off: the static sample split for launches of few tiles, as
+// before), RTCLJ_THIEVES (helper workgroups per workgroup slot of the
+// device), RTCLJ_STEAL_MIN (unclaimed samples a tile needs for a helper to join)
+static int env_int(const char* name, int dflt, int lo) {
+  const char* e = std::getenv(name);
+  return e ? std::max(lo, std::atoi(e)) : dflt;
+}
+static int split_rounds() { return env_int("RTCLJ_SPLIT_ROUNDS", 3, 1); }   // (kSplitRounds above)
+
+// workgroups device `device` holds at once for kernel fn with `lds` bytes of
+// dynamic LDS (CUs x the occupancy query), cached per (device, fn, lds)
+static int launch_slots(int device, const void* fn, size_t lds, int threads = 256) {
+  struct Entry { int device; const void* fn; size_t lds; int slots; };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Entry& e : cache)
+    if (e.device == device && e.fn == fn && e.lds == lds) return e.slots;
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess)
+    return 0;
+  cache.push_back({device, fn, lds, cus * per});
+  return cus * per;
+}
+
+// the variants of the compact image (u8 node-index stack, u32 sums)
+static bool compact_variant(int v) { return v == 22 || v == 24 || v == 26 || v == 28; }
+
 // selector -> the variant a launch on ds runs
 static int resolve_variant(const rt_dscene& ds, int vsel) {
   // default: 4-body leaves, unless that tree's LDS image limits a CU below
   // 5 workgroups (160 KB / 5) and the 8-body-leaf tree's is smaller
-  // (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2)
+  // (measured: 1025 bodies 12.9 vs 14.0 ms; 484: 10.8 vs 12.2); each image
+  // with the stack rows of its own variant's workgroup (18: 512 lanes)
   if (vsel == 0)
     vsel = (lds_of(ds.tree[1], 1) > kLds5 && ds.tree[2].n_nodes <= 256 &&
-            lds_of(ds.tree[2], 2) < lds_of(ds.tree[1], 1)) ? 18 : 16;
+            lds_of(ds.tree[2], 2, variant_table(18).threads) < lds_of(ds.tree[1], 1)) ? 18 : 16;
   if ((vsel == 18 || vsel == 19) && ds.tree[2].n_nodes > 256) vsel -= 2;   // u8 stack: 256 nodes at most
   // u16 stack of node LDS addresses: the kernel's static LDS (< 4 KB; 8 KB
   // allowed for) plus the node region must stay below 64 KB
@@ -620,10 +658,12 @@ static int resolve_variant(const rt_dscene& ds, int vsel) {
   if (vsel >= 11) {
     const DTree& t = ds.tree[variant_tree(vsel)];
     if (t.depth + 2 > kBvhStack) return 5;                       // tree too deep for the stack
-    if (vsel != 12 && lds_of(t, variant_tree(vsel)) > 96 * 1024) vsel = 12;          // tree too big for LDS: 2-body leaves, global
+    // (the stack rows of the variant's own workgroup size, as launch_lds)
+    if (vsel != 12 && lds_of(t, variant_tree(vsel), variant_table(vsel).threads) > 96 * 1024)
+      vsel = 12;   // tree too big for LDS: 2-body leaves, global
     if (vsel == 12 && ds.tree[0].depth + 2 > kBvhStack) return 5;
   }
-  if ((vsel == 22 || vsel == 24 || vsel == 26) && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
+  if (compact_variant(vsel) && ds.tree[1].n_nodes > 256) vsel = 16;   // (u8 node indices)
   return vsel;
 }
 
@@ -658,7 +698,23 @@ static int launch_variant(const rt_dscene& ds, const rt_params& p) {
     else if (lds_of_compact(ds.tree[1], 512) + kStaticLds8 <= 160 * 1024 / 3)
       vsel = 24;
   }
-  if ((vsel == 24 || vsel == 26) && !compact_ok(ds, p)) vsel = 16;
+  if ((vsel == 24 || vsel == 26 || vsel == 28) && !compact_ok(ds, p)) vsel = 16;
+  // A launch of 22 with few 8 x 8 tiles -- fewer than kWholeTh4 (RTCLJ_TH4,
+  // default 2; 0: never) x the workgroups the device holds, a shard of a
+  // multi-GPU frame -- runs 28: the same image on 8 x 4-pixel pools, whole,
+  // where 22 would split every tile's samples over 2-3 workgroups (each
+  // split re-loads the tree, drains its own pool and adds its sums through
+  // HBM atomics and finalize_kernel).  DESIGN.md §6.
+  if (sel == 0 && vsel == 22) {
+    const int ratio = env_int("RTCLJ_TH4", 2, 0);
+    if (ratio > 0) {
+      const int rows = rows_out(p);
+      const int64_t n8 = static_cast<int64_t>((p.width + kTile - 1) / kTile) * ((rows + kTile - 1) / kTile);
+      const Variant& v22 = variant_table(22);
+      const int slots = launch_slots(ds.device, v22.fn, lds_of_compact(ds.tree[1], v22.threads), v22.threads);
+      if (slots > 0 && n8 < static_cast<int64_t>(ratio) * slots) vsel = 28;
+    }
+  }
   return vsel;
 }
 
@@ -668,7 +724,7 @@ extern "C" int rt_resolve_variant(const rt_dscene* ds) { return ds ? resolve_var
 static size_t launch_lds(const rt_dscene& ds, int vsel) {
   const Variant& v = variant_table(vsel);
   if (v.scan == SCAN_BVHS) return static_cast<size_t>(ds.tree[1].blob_f4) * 16 + kXBytes;   // blob | exchange
-  if (vsel == 22 || vsel == 24 || vsel == 26) return lds_of_compact(ds.tree[1], v.threads);
+  if (compact_variant(vsel)) return lds_of_compact(ds.tree[1], v.threads);
   if (vsel >= 11) {
     const DTree& tr = ds.tree[variant_tree(vsel)];
     return v.lds ? lds_of(tr, variant_tree(vsel), v.threads) : stack_of(tr, variant_tree(vsel), v.threads);
@@ -727,33 +783,6 @@ static uint64_t magic64(int d) { return d <= 1 ? 0 : ~0ull / static_cast<uint64_
 // 5.72x at 4, 5.30x at 6, 3.96x at 16; unsplit 2.57x)
 constexpr int kSplitMax = 64;
 
-// Tile sharing (DESIGN.md §3.1), A/B knobs read at every launch:
-// RTCLJ_STEAL=0 (off: the static sample split for launches of few tiles, as
-// before), RTCLJ_THIEVES (helper workgroups per workgroup slot of the
-// device), RTCLJ_STEAL_MIN (unclaimed samples a tile needs for a helper to join)
-static int env_int(const char* name, int dflt, int lo) {
-  const char* e = std::getenv(name);
-  return e ? std::max(lo, std::atoi(e)) : dflt;
-}
-static int split_rounds() { return env_int("RTCLJ_SPLIT_ROUNDS", 3, 1); }   // (kSplitRounds above)
-
-// workgroups device `device` holds at once for kernel fn with `lds` bytes of
-// dynamic LDS (CUs x the occupancy query), cached per (device, fn, lds)
-static int launch_slots(int device, const void* fn, size_t lds, int threads = 256) {
-  struct Entry { int device; const void* fn; size_t lds; int slots; };
-  static std::mutex mu;
-  static std::vector<Entry> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const Entry& e : cache)
-    if (e.device == device && e.fn == fn && e.lds == lds) return e.slots;
-  int cus = 0, per = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess)
-    return 0;
-  cache.push_back({device, fn, lds, cus * per});
-  return cus * per;
-}
-
 namespace rtclj {
 int fill_async(void* p, int byte_value, size_t bytes, void* stream) {
   if (bytes == 0) return hipSuccess;
@@ -789,7 +818,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   clear_error();
   if (!ds || !c || !p || !d_out) return set_error(RT_E_ARG, "rt_launch: NULL argument");
   if (p->width <= 0 || p->height <= 0 || p->spp < 0 || p->spp > RT_MAX_SPP ||
-      (p->flags & ~(RT_FLAG_REALM | RT_FLAG_STREAMED)) != 0)
+      (p->flags & ~(RT_FLAG_REALM | RT_FLAG_STREAMED | RT_FLAG_REJECTION_SAMPLERS)) != 0)
     return set_error(RT_E_ARG, "rt_launch: bad width/height/spp/flags");
   const int rows = rows_out(*p);
   if (rows < 0) return set_error(RT_E_ARG, "rt_launch: bad row selection");
@@ -820,6 +849,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   a.sample_begin = p->sample_begin;
   a.max_depth = p->max_depth;
   a.realm = (p->flags & RT_FLAG_REALM) ? 1 : 0;
+  // the loop-free samplers unless the caller asks for the reference's rejection loops
+  a.sampler = (p->flags & RT_FLAG_REJECTION_SAMPLERS) ? 0 : (RT_SAMPLER_SPHERE | RT_SAMPLER_DISK);
   a.key = seed_key(p->seed);
   if (rows == 0) return RT_OK;
   HIP_TRY(hipSetDevice(ds->device));
@@ -837,7 +868,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // entries per lane: the ordered traversal (trees 1, 2) holds at most depth
   // (a node on level L has L - 1 ancestors; the dead far-child write goes one
   // above them); tree 0 also serves the while-while variants (depth + 2)
-  a.bvh_stack = vsel == 22 || vsel == 24 || vsel == 26 ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
+  a.bvh_stack = compact_variant(vsel) ? stack_entries_compact(tr) : stack_entries(tr, variant_tree(vsel));
   for (int k = 0; k < 3; ++k) a.bvh_c[k] = tr.c[k];
   a.bvh_r = tr.r;
   // drain compaction: a post holds as many paths as a wave's stack slice has
@@ -848,7 +879,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     a.compact = is_bvh_scan(v.scan) ? std::min(a.mb_paths, env_int("RTCLJ_COMPACT", a.mb_paths, 0)) : 0;
   }
   hipStream_t stream = static_cast<hipStream_t>(hip_stream);
-  const int th = tile_rows(v.scan);   // the variant's tile rows
+  const int th = variant_rows(v);   // the variant's tile rows
   const int gx = (p->width + kTile - 1) / kTile, gy = (rows + th - 1) / th;
   const dim3 block(v.threads);
   const int n_tiles = gx * gy;
@@ -907,7 +938,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       split = std::max(1, std::atoi(e));
     } else {
       const int slots = launch_slots(ds->device, v.fn, lds, v.threads);
-      const int64_t want = static_cast<int64_t>(split_rounds()) * slots;
+      // (28: its pools are the split's answer already; they split only when
+      // fewer than RTCLJ_TH4_SPLIT_ROUNDS (1) rounds of them fill the device)
+      const int rounds = vsel == 28 ? env_int("RTCLJ_TH4_SPLIT_ROUNDS", 1, 1) : split_rounds();
+      const int64_t want = static_cast<int64_t>(rounds) * slots;
       if (slots > 0 && n_tiles < want) {
         split = static_cast<int>((want + n_tiles - 1) / n_tiles);
         // frames in flight: the next frame fills this launch's tail, so two

@@ -287,10 +287,14 @@ __global__ __launch_bounds__(kSortThreads, 6) void sorted_kernel(const KArgs a) 
       const float sz = fmaf(a.cam[11], fy, fmaf(a.cam[8], fx, a.cam[5]));
       if (a.defocus) {
         float qx, qy2;
-        do {
-          qx = rng_sym(st);
-          qy2 = rng_sym(st);
-        } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        if (a.sampler & RT_SAMPLER_DISK) {
+          disk_direct(st, qx, qy2);
+        } else {
+          do {
+            qx = rng_sym(st);
+            qy2 = rng_sym(st);
+          } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        }
         ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
         oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
         oz = fmaf(a.cam[17], qy2, fmaf(a.cam[14], qx, cz));
@@ -464,7 +468,10 @@ __global__ __launch_bounds__(kSortThreads, 6) void sorted_kernel(const KArgs a) 
       last = best;
       if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
         float qx, qy, qz;
-        random_unit<false>(st, qx, qy, qz);
+        if (a.sampler & RT_SAMPLER_SPHERE)
+          sphere_direct(st, qx, qy, qz);
+        else
+          random_unit<false>(st, qx, qy, qz);
         if (kind == RT_LAMBERTIAN) {
           float sx = qx + nx, sy = qy + ny, sz = qz + nz;
           if (!a.realm && fabsf(sx) < 1e-8f && fabsf(sy) < 1e-8f && fabsf(sz) < 1e-8f) {

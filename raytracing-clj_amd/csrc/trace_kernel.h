@@ -108,6 +108,7 @@ struct alignas(16) KArgs {
   uint64_t rt_magic;         // d = row_tile
   int spp, sample_begin, max_depth;
   int realm;             // RT_FLAG_REALM semantics (uniform)
+  int sampler;           // RT_SAMPLER_* bits: the loop-free samplers (uniform)
   uint32_t key;
   // Tile sharing.  Workgroups [0, n_units) run the units
   // (dispatch positions); the grid's last workgroups are helpers,
@@ -207,6 +208,73 @@ __device__ __forceinline__ void random_unit(uint32_t& s, float& x, float& y, flo
   x = x * il;
   y = y * il;
   z = z * il;
+}
+
+// ---- Loop-free samplers (RT_FLAG_DIRECT_SAMPLERS) ----
+enum { RT_SAMPLER_SPHERE = 1, RT_SAMPLER_DISK = 2 };   // KArgs::sampler bits
+// The same distributions as vec3a/random-unit-vec3 (uniform on the unit
+// sphere) and vec3a/random-in-unit-disk (uniform in the unit disk), drawn
+// with a fixed number of draws instead of a rejection loop, so a wave no
+// longer pays for its slowest lane's trips.  Fixed fp32 op sequences with no
+// hardware transcendental (the oracle's MODE_MIRROR32 | ORACLE_DIRECT restates
+// them op for op):
+//   sphere (Archimedes): z = 2 xi1 - 1, r = sqrt(1 - z^2), phi = 2 pi xi2;
+//   disk: r = sqrt(xi1), phi = 2 pi xi2;
+// (cos phi, sin phi) from the 24-bit integer of xi2: the nearest quarter turn
+// q, the rest as theta in [-pi/4, pi/4) by Taylor polynomials to theta^9 /
+// theta^8 (|error| < 3e-8), rotated by q.
+__device__ __forceinline__ uint32_t rng_u24(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return s >> 8;
+}
+__device__ __forceinline__ void turn24(uint32_t u, float r, float& x, float& y) {
+  const int f = static_cast<int>(u << 10) >> 10;             // the low 22 bits, signed: [-2^21, 2^21)
+  const uint32_t q = (u + 0x200000u) >> 22;                  // nearest quarter turn (mod 4 below)
+  const float th = static_cast<float>(f) * 0x1.921fb6p-22f;  // f * RN(2 pi / 2^24): |th| <= pi/4
+  const float t2 = th * th;
+  float ps = fmaf(t2, 0x1.71de3ap-19f, -0x1.a01a02p-13f);    // 1/9!, -1/7!
+  ps = fmaf(t2, ps, 0x1.111112p-7f);                         // 1/5!
+  ps = fmaf(t2, ps, -0x1.555556p-3f);                        // -1/3!
+  const float sn = fmaf(th * t2, ps, th);
+  float pc = fmaf(t2, 0x1.a01a02p-16f, -0x1.6c16c2p-10f);    // 1/8!, -1/6!
+  pc = fmaf(t2, pc, 0x1.555556p-5f);                         // 1/4!
+  pc = fmaf(t2, pc, -0.5f);
+  const float cs = fmaf(t2, pc, 1.0f);
+  // q quarter turns: (cs, sn) -> (-sn, cs) -> (-cs, -sn) -> (sn, -cs); the
+  // signs ride on r (x = (+-r) * a: the same bits as -(r * a))
+  const bool sw = (q & 1u) != 0;
+  const float a = sw ? sn : cs, b = sw ? cs : sn;
+  const float rx = __uint_as_float(__float_as_uint(r) ^ (((q + 1u) & 2u) << 30));
+  const float ry = __uint_as_float(__float_as_uint(r) ^ ((q & 2u) << 30));
+  x = rx * a;
+  y = ry * b;
+}
+template <bool STATS = false>
+__device__ __forceinline__ void sphere_direct(uint32_t& s, float& x, float& y, float& z, uint64_t* trips = nullptr,
+                                              uint64_t* flops = nullptr) {
+  if constexpr (STATS) {
+    wave_event(*trips);
+    *flops += 24;   // 2 xi - 1, 1 - z^2, sqrt, th, polynomials (17), 2 x r * a
+  }
+  z = rng_sym(s);
+  // 1 - z^2 in one rounding; z is a multiple of 2^-23 in [-1, 1), so the
+  // operand is 0 or >= 2^-22: sqrt_rn_normal's range, 0 included (sqrt 0 = 0
+  // and both neighbour residuals fail their tests)
+  const float r = sqrt_rn_normal(fmaf(-z, z, 1.0f));
+  turn24(rng_u24(s), r, x, y);
+}
+template <bool STATS = false>
+__device__ __forceinline__ void disk_direct(uint32_t& s, float& x, float& y, uint64_t* trips = nullptr,
+                                            uint64_t* flops = nullptr) {
+  if constexpr (STATS) {
+    wave_event(*trips);
+    *flops += 22;
+  }
+  // xi1 is 0 or >= 2^-24: sqrt_rn_normal's range, 0 included
+  const float r = sqrt_rn_normal(rng_uniform(s));
+  turn24(rng_u24(s), r, x, y);
 }
 
 // A sample's colour channel in the pixel's fixed-point sum: c * 2^24
@@ -382,7 +450,9 @@ __device__ void diag_scan(const struct KArgs& a, const float4* s_geo, float ox, 
 // NW waves per workgroup (4; 8 or 16 for trees whose large LDS image more
 // waves share: C4's 1000-body tree as the compact 4-body image, two 16-wave
 // workgroups = 8 waves per SIMD, where 4-wave workgroups fit 3 per CU)
-template <int SRC, int SCAN, bool STATS = false, int NW = 4>
+// THT: the pool's tile rows (0: tile_rows(SCAN); variant 28 runs 22's
+// compact image on 8 x 4-pixel pools, for launches of few 8 x 8 tiles)
+template <int SRC, int SCAN, bool STATS = false, int NW = 4, int THT = 0>
 __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_kernel(const KArgs a) {
   constexpr int NT = 64 * NW;   // threads
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
@@ -390,7 +460,8 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // j / npx: the lanes ending paths together add into different pixels'
   // sums).  A lane whose path ends takes the next index from an LDS counter
   // (one ds_add per wave event, then an mbcnt prefix).  The colour sums are
-  // u64 per pixel and channel in LDS, added with ds_add_u64: order-free.
+  // integers per pixel and channel in LDS (u64, ds_add_u64; the compact
+  // variants: u32 with counted wraps, below): order-free.
   //
   // The workgroup's unit: a whole tile (owner) or one sample split of a
   // tile, or -- a helper -- a share of another workgroup's tile (DESIGN.md
@@ -409,11 +480,13 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   __shared__ int s_mb_post[NW], s_mb_take[NW], s_alive, s_mb_avail;
   // per wave: post when down to this many paths (0: posted once already; -1: off)
   __shared__ int s_mb_lim[NW];
-  constexpr int TH = tile_rows(SCAN);   // tile rows
+  constexpr int TH = THT ? THT : tile_rows(SCAN);   // tile rows
   constexpr int NPX = kTile * TH;       // pool pixels
-  // the pool's pixel sums: u32 in the compact variant (the host runs it only
-  // when a sample's colour is <= 1 per channel and spp <= 255: a sum stays
-  // below 255 * 2^24 < 2^32), u64 otherwise
+  // the pool's pixel sums: u32 in the compact variants (the host runs them
+  // only when a sample's colour is <= 1 per channel and spp < 65536: a
+  // sample adds at most 2^24 per channel, so a channel's sum wraps past 2^32
+  // at most spp / 256 < 256 times, and the wraps are counted in a byte per
+  // channel, s_carry, when spp > 255), u64 otherwise
   using AccT = std::conditional_t<SCAN == SCAN_BVHQ7, unsigned, unsigned long long>;
   __shared__ AccT s_acc[NPX * 3];
   uint64_t st_iter = 0, st_lanes = 0, st_sph = 0, st_blk = 0, st_blk_lanes = 0;
@@ -875,14 +948,18 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       if (a.defocus) {
         // defocus-disk-sample + random-in-unit-disk (raytracing.clj:89-93, vec3a.clj:81-86)
         float qx, qy2;
-        do {
-          if constexpr (STATS) {
-            wave_event(st_disk);
-            st_fl += 7;   // 2 x (2 xi - 1) + |q|^2
-          }
-          qx = rng_sym(st);
-          qy2 = rng_sym(st);
-        } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        if (a.sampler & RT_SAMPLER_DISK) {
+          disk_direct<STATS>(st, qx, qy2, &st_disk, &st_fl);
+        } else {
+          do {
+            if constexpr (STATS) {
+              wave_event(st_disk);
+              st_fl += 7;   // 2 x (2 xi - 1) + |q|^2
+            }
+            qx = rng_sym(st);
+            qy2 = rng_sym(st);
+          } while (!(fmaf(qy2, qy2, qx * qx) < 1.0f));
+        }
         if constexpr (STATS) st_fl += 12;
         ox = fmaf(a.cam[15], qy2, fmaf(a.cam[12], qx, cx));
         oy = fmaf(a.cam[16], qy2, fmaf(a.cam[13], qx, cy));
@@ -1384,7 +1461,10 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         // the segment for these lanes): a wave loops the rejection sampler
         // once for both kinds
         float qx, qy, qz;
-        random_unit<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
+        if (a.sampler & RT_SAMPLER_SPHERE)
+          sphere_direct<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
+        else
+          random_unit<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
         if constexpr (STATS) st_fl += kind == RT_LAMBERTIAN ? 6 : 26;
         if (kind == RT_LAMBERTIAN) {
           // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
@@ -1739,11 +1819,14 @@ struct Variant {
   const void* fn;
   bool lds;
   bool stats;
-  int scan;   // SCAN_* (the tile shape: tile_rows)
+  int scan;   // SCAN_* (the tile shape: tile_rows, unless th)
   int threads = 256;   // workgroup size
+  int th = 0;          // the pool's tile rows (0: tile_rows(scan))
 };
+inline int variant_rows(const Variant& v) { return v.th ? v.th : tile_rows(v.scan); }
 #define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
 #define RT_KW(SRC, SCAN, ST, NW) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST, NW>)
+#define RT_KWT(SRC, SCAN, ST, NW, TH) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST, NW, TH>)
 // The diagnostic library's variants (trace_diag.hip): v's entry, or NULL.
 const Variant* diag_variant(int v);
 

@@ -30,33 +30,43 @@
         (aset mat (+ 3 (* 4 i)) (float (or (:fuzz material) (:refraction-index material) 0.0)))))
     [sph knd mat]))
 
+(defn- flags
+  "rt_params.flags of an options map: :realm? (RT_FLAG_REALM) and
+  :rejection-samplers? (RT_FLAG_REJECTION_SAMPLERS: vec3a's own rejection
+  loops instead of the kernel's loop-free samplers of the same distributions)."
+  [{:keys [realm? rejection-samplers?]}]
+  (bit-or (if realm? Native/FLAG_REALM 0) (if rejection-samplers? Native/FLAG_REJECTION_SAMPLERS 0)))
+
 (defn render
   "width*height*3 linear RGB floats: compute-pixel's accum/spp for every pixel.
   camera keys are the values -main derives (raytracing.clj:126-139).
   :realm? true renders with realm.raytracing's semantics (RT_FLAG_REALM:
   src/realm/raytracing.clj; pass realm's camera: no defocus, focal length
-  |look-from - look-at|)."
+  |look-from - look-at|).  :rejection-samplers? true draws vec3a's
+  random-unit-vec3 / random-in-unit-disk by their rejection loops
+  (RT_FLAG_REJECTION_SAMPLERS); the default draws the same distributions
+  loop-free."
   [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
-   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
+   {:keys [width height samples-per-px max-depth seed gpus] :or {seed 1 gpus 0} :as opts}]
   (let [[sph knd mat] (flatten-bodies bodies)
         cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))
         out (float-array (* width height 3))]
     (Native/renderWithFlags sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
                             samples-per-px max-depth (long seed) (int gpus)
-                            (if realm? Native/FLAG_REALM 0) out)
+                            (flags opts) out)
     out))
 
 (defn render-bytes
   "render, then write-color! on the device (rt_render_u8): width*height*3
   bytes, the 0..255 values -main writes (raytracing.clj:19-26)."
   [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
-   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
+   {:keys [width height samples-per-px max-depth seed gpus] :or {seed 1 gpus 0} :as opts}]
   (let [[sph knd mat] (flatten-bodies bodies)
         cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))
         out (byte-array (* width height 3))]
     (Native/renderBytes sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
                         samples-per-px max-depth (long seed) (int gpus)
-                        (if realm? Native/FLAG_REALM 0) out)
+                        (flags opts) out)
     out))
 
 (defn submit-bytes
@@ -65,12 +75,12 @@
   next before it awaits the last, as the executor's futures do
   (raytracing.clj:157-171)."
   [bodies {:keys [center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v defocus-angle]}
-   {:keys [width height samples-per-px max-depth seed gpus realm?] :or {seed 1 gpus 0}}]
+   {:keys [width height samples-per-px max-depth seed gpus] :or {seed 1 gpus 0} :as opts}]
   (let [[sph knd mat] (flatten-bodies bodies)
         cam (float-array (concat center pixel-00-loc pixel-du pixel-dv defocus-disk-u defocus-disk-v))]
     {:handle (Native/submitBytes sph knd mat cam (if (pos? (or defocus-angle 0)) 1 0) width height
                                  samples-per-px max-depth (long seed) (int gpus)
-                                 (if realm? Native/FLAG_REALM 0))
+                                 (flags opts))
      :size (* width height 3)}))
 
 (defn await-bytes

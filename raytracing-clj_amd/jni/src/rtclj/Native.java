@@ -13,12 +13,14 @@ public final class Native {
                                   int width, int height, int spp, int depth, long seed, int nGpus,
                                   float[] outRgb);
 
-  /** render with rt_params.flags (RT_FLAG_REALM = 2: the realm.raytracing semantics). */
+  /** render with rt_params.flags (RT_FLAG_REALM = 2: the realm.raytracing semantics;
+   *  RT_FLAG_REJECTION_SAMPLERS = 8: vec3a's rejection-loop samplers). */
   public static native int renderWithFlags(float[] spheres, int[] kinds, float[] mats, float[] camera,
                                            int defocus, int width, int height, int spp, int depth, long seed,
                                            int nGpus, int flags, float[] outRgb);
 
   public static final int FLAG_REALM = 2;
+  public static final int FLAG_REJECTION_SAMPLERS = 8;
 
   /** render + write-color! on the device (rt_render_u8): rows x width x 3 bytes. */
   public static native int renderBytes(float[] spheres, int[] kinds, float[] mats, float[] camera, int defocus,

@@ -23,6 +23,7 @@ RT_MAX_SPP = 1 << 24
 RT_FLAG_SHARDS_ON_DEVICE0 = 1
 RT_FLAG_REALM = 2
 RT_FLAG_STREAMED = 4
+RT_FLAG_REJECTION_SAMPLERS = 8   # vec3a.clj:74-86's rejection loops instead of the loop-free samplers
 
 
 class RTError(RuntimeError):

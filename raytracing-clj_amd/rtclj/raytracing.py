@@ -248,9 +248,10 @@ def read_ppm(path) -> np.ndarray:
     return np.array(tok[4:4 + w * h * 3], np.int64).astype(np.uint8).reshape(h, w, 3)
 
 
-def main(*args, out_path="scene.ppm", seed: int = 1, n_devices: int = 0) -> np.ndarray:
+def main(*args, out_path="scene.ppm", seed: int = 1, n_devices: int = 0, flags: int = 0) -> np.ndarray:
     """-main [spp] [depth] (raytracing.clj:95-177): render the five-body scene
-    at 400 x 225 and write `out_path` (PPM P3).  Returns the uint8 image."""
+    at 400 x 225 and write `out_path` (PPM P3).  Returns the uint8 image.
+    flags: rt_params.flags (e.g. RT_FLAG_REJECTION_SAMPLERS)."""
     spp = int(args[0]) if len(args) > 0 and args[0] is not None else 100
     max_depth = int(args[1]) if len(args) > 1 and args[1] is not None else 50
     print("config:", {"samples-per-px": spp, "max-depth": max_depth})
@@ -258,7 +259,7 @@ def main(*args, out_path="scene.ppm", seed: int = 1, n_devices: int = 0) -> np.n
     width = 400
     height = image_height(width)
     cam = camera(width, height, **REFERENCE_CAMERA)
-    lin = render(hittables, cam, width, height, spp, max_depth, seed=seed, n_devices=n_devices)
+    lin = render(hittables, cam, width, height, spp, max_depth, seed=seed, n_devices=n_devices, flags=flags)
     rgb = write_color(lin)
     write_ppm(out_path, rgb)
     print(f'"Elapsed time: {(time.perf_counter() - t0) * 1e3:.3f} msecs"')

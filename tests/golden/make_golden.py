@@ -14,7 +14,10 @@ where /root/reference exists; nothing at test time reads /root/reference).
                          computed here in pure Python
   mirror_small.npz       small renders by the oracle's fp32 kernel mirror
                          (regression pins for the oracle and the GPU path),
-                         incl. one in realm semantics (MODE_REALM32)
+                         incl. one in realm semantics (MODE_REALM32), with
+                         the reference's rejection samplers
+  mirror_small_direct.npz  the same renders with the kernel's default
+                         loop-free samplers (oracle mode | DIRECT)
   scene_realm_ppm.npz    the reference's realm.raytracing output,
   scene_realm_ppm_stats.json   scene-realm.ppm (`clojure -M:realm`: 400x225,
                          100 spp, depth 50), pixels and the same statistics
@@ -22,7 +25,7 @@ where /root/reference exists; nothing at test time reads /root/reference).
                          by tests/pngdec.py: header, row filters, sha256 of
                          the decoded pixels, and whether they equal scene.ppm's
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--mirror-only]
 """
 from __future__ import annotations
 
@@ -285,28 +288,43 @@ def main():
     rng = [{"seed": s, "pixel": p, "sample": k, "draws": stream(s, p, k, 8)}
            for s, p, k in [(1, 0, 0), (1, 0, 1), (1, 1, 0), (7, 12345, 99), (2**40 + 3, 810000 - 1, 1999)]]
     (HERE / "rng_golden.json").write_text(json.dumps(rng, indent=1))
-    # small fp32-mirror renders (regression pins; oracle = test infrastructure)
+    mirror_fixtures()
+    print("kats, rng, mirror fixtures written")
+
+
+def mirror_fixtures():
+    """Small fp32-mirror renders (regression pins; oracle = test
+    infrastructure): mirror_small.npz with the reference's rejection samplers
+    (the kernel's RT_FLAG_REJECTION_SAMPLERS), mirror_small_direct.npz with the
+    kernel's default loop-free samplers (oracle mode | DIRECT)."""
     sys.path[:0] = [str(ROOT), str(ROOT / "raytracing-clj_amd")]
     import oracle
+    for direct, name in ((0, "mirror_small.npz"), (oracle.DIRECT, "mirror_small_direct.npz")):
+        _mirror_fixture(oracle, direct, name)
+
+
+def _mirror_fixture(oracle, direct, name):
     from rtclj import raytracing as R
     from rtclj import scenes
     sc = R.Scene.from_bodies(R.hittables)
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
-    ref, _, segs_r, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+    ref, _, segs_r, _ = oracle.render(oracle.MODE_MIRROR32 | direct, sc.sphere.astype(np.float64), sc.kind,
                                       sc.mat.astype(np.float64), cam.as_list(), cam.defocus, 48, 27, 8, 50, seed=3)
     cs = scenes.cover(11)
     cc = scenes.cover_camera(32, 18)
-    cov, _, segs_c, _ = oracle.render(oracle.MODE_MIRROR32, cs.sphere.astype(np.float64), cs.kind,
+    cov, _, segs_c, _ = oracle.render(oracle.MODE_MIRROR32 | direct, cs.sphere.astype(np.float64), cs.kind,
                                       cs.mat.astype(np.float64), cc.as_list(), cc.defocus, 32, 18, 4, 50, seed=5)
     from rtclj import realm
     rs = R.Scene.from_bodies(realm.hittables)
     rc = realm.camera(48, 27)
-    rlm, _, segs_m, _ = oracle.render(oracle.MODE_REALM32, rs.sphere.astype(np.float64), rs.kind,
+    rlm, _, segs_m, _ = oracle.render(oracle.MODE_REALM32 | direct, rs.sphere.astype(np.float64), rs.kind,
                                       rs.mat.astype(np.float64), rc.as_list(), rc.defocus, 48, 27, 8, 50, seed=3)
-    np.savez_compressed(HERE / "mirror_small.npz", reference_48x27_spp8_seed3=ref, cover_32x18_spp4_seed5=cov,
+    np.savez_compressed(HERE / name, reference_48x27_spp8_seed3=ref, cover_32x18_spp4_seed5=cov,
                         realm_48x27_spp8_seed3=rlm, segments=np.array([segs_r, segs_c, segs_m], np.int64))
-    print("kats, rng, mirror fixtures written")
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--mirror-only"]:   # the mirror fixtures alone (no reference files read)
+        mirror_fixtures()
+    else:
+        main()

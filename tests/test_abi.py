@@ -66,6 +66,20 @@ def test_abi_revision_matches_header():
     assert f"abi {RT_ABI_VERSION}" in rtclj.lib.rt_version().decode()
 
 
+def test_flag_values_match_header():
+    """rt.h's RT_FLAG_* == the Python binding's == the JNI side's Native.FLAG_*
+    (the Clojure ns passes Native's constants)."""
+    from rtclj import _lib
+    hdr = (ROOT / "include" / "rt.h").read_text()
+    flags = {k: int(v) for k, v in re.findall(r"#define RT_FLAG_(\w+) (\d+)", hdr)}
+    assert set(flags) == {"SHARDS_ON_DEVICE0", "REALM", "STREAMED", "REJECTION_SAMPLERS"}
+    for k, v in flags.items():
+        assert getattr(_lib, "RT_FLAG_" + k) == v, k
+    java = (ROOT / "raytracing-clj_amd" / "jni" / "src" / "rtclj" / "Native.java").read_text()
+    jflags = {k: int(v) for k, v in re.findall(r"static final int FLAG_(\w+) = (\d+);", java)}
+    assert jflags == {"REALM": flags["REALM"], "REJECTION_SAMPLERS": flags["REJECTION_SAMPLERS"]}
+
+
 def test_no_gpu_here_fails_loudly():
     from rtclj import RTError
     from rtclj import raytracing as R
@@ -98,7 +112,7 @@ def test_argument_errors():
     p_short = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=1, max_depth=5)
     assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_short), fp, 10, None) == -1
     assert b"out_len" in lib.rt_last_error()
-    p_flag = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=1, max_depth=5, flags=8)
+    p_flag = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=1, max_depth=5, flags=16)   # (an unknown bit)
     assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_flag), fp, out.size, None) == -1
     p_spp = rt_params(width=16, height=9, row_begin=0, row_end=9, spp=(1 << 24) + 1, max_depth=5)
     assert lib.rt_render(C.byref(sc.c), C.byref(cam), C.byref(p_spp), fp, out.size, None) == -1

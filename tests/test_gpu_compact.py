@@ -4,7 +4,7 @@ its traversal stack's LDS and leaves; its sibling waves' free lanes take
 them and run them to the end.  A path carries everything it needs (origin,
 direction, throughput, RNG state, pool pixel, depth left, the body it
 leaves) and the colour sums are integers, so every frame must equal the
-oracle's fp32 mirror (MODE_MIRROR32) bit for bit whoever finishes which
+oracle's fp32 mirror (MODE_MIRROR32 | DIRECT) bit for bit whoever finishes which
 path -- at every threshold, with and without tile sharing and sample splits,
 on pools smaller than a workgroup's 256 lanes (fewer waves start) and on
 C4's 8-body-leaf traversal (u8 stack: smaller posts).
@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _mirror(sc, cam, w, h, spp, depth, seed):
-    out, _, _, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+    out, _, _, _ = oracle.render(oracle.MODE_MIRROR32 | oracle.DIRECT, sc.sphere.astype(np.float64), sc.kind,
                                  sc.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
                                  seed=seed)
     return out
@@ -52,14 +52,15 @@ def cover(gpu_lib):
                                    dict(RTCLJ_COMPACT="5", RTCLJ_SPLIT="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_SPLIT="1", RTCLJ_STEAL_MIN="1", RTCLJ_SHARE_RECORDED="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_STEAL="0"),
-                                   dict(RTCLJ_COMPACT="0")])
+                                   dict(RTCLJ_COMPACT="0"), dict(RTCLJ_TH4="0"), dict(RTCLJ_COMPACT="1", RTCLJ_TH4="0")])
 def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
     """Thresholds 64 (clamped: posts as full as the stack slice holds, 22 on
     this scene's tree), 16, 1 and 5; tiles kept whole and shared
     (RTCLJ_SPLIT=1, helpers joining any tile), sharing off, compaction off;
     frames of many small pools, few large ones (sample splits by default) and
     pools of 1..255 samples: each launched twice (plain order, then the
-    recorded one), every frame equal to the mirror."""
+    recorded one), every frame equal to the mirror.  These small frames run
+    28 (8 x 4-pixel pools) by default; RTCLJ_TH4=0 keeps them on 22."""
     from rtclj import scenes
     sc, ds = cover
     for k, v in knobs.items():

@@ -63,7 +63,7 @@ def test_rt_main_reference_scene_equals_mirror(gpu_lib, tmp_path):
     assert img.shape == (225, 400, 3)
     sc = R.Scene.from_bodies(R.hittables)
     cam = R.camera(400, 225, **R.REFERENCE_CAMERA)
-    ref, sps = _mirror_q8(oracle.MODE_MIRROR32, sc, cam, 400, 225, 16, 50, seed=1)
+    ref, sps = _mirror_q8(oracle.MODE_MIRROR32 | oracle.DIRECT, sc, cam, 400, 225, 16, 50, seed=1)
     assert np.array_equal(img, ref)
     assert abs(_segs_per_sample(out) - sps) < 1e-3
     assert np.array_equal(decode((tmp_path / "scene.png").read_bytes())[0], img)
@@ -81,7 +81,7 @@ def test_rt_main_realm_equals_mirror(gpu_lib, tmp_path):
     w, h = 400, realm.image_height(400)
     assert img.shape == (h, w, 3) == (224, 400, 3)
     sc = R.Scene.from_bodies(realm.hittables)
-    ref, _ = _mirror_q8(oracle.MODE_REALM32, sc, realm.camera(w, h), w, h, 8, 50, seed=1)
+    ref, _ = _mirror_q8(oracle.MODE_REALM32 | oracle.DIRECT, sc, realm.camera(w, h), w, h, 8, 50, seed=1)
     assert np.array_equal(img, ref)
 
 
@@ -94,7 +94,7 @@ def test_rt_main_cover_scene(gpu_lib, tmp_path):
     out = _run(["4", "50", "--scene", "cover", "--width", "160", "--seed", "9", "--out", "c.ppm", "--json"], tmp_path)
     img = R.read_ppm(tmp_path / "c.ppm")
     h = R.image_height(160)
-    ref, _ = _mirror_q8(oracle.MODE_MIRROR32, scenes.cover(11), scenes.cover_camera(160, h), 160, h, 4, 50, seed=9)
+    ref, _ = _mirror_q8(oracle.MODE_MIRROR32 | oracle.DIRECT, scenes.cover(11), scenes.cover_camera(160, h), 160, h, 4, 50, seed=9)
     assert np.array_equal(img, ref)
     # like -main's (ppm->png "scene.ppm" "scene.png") (raytracing.clj:176): the
     # PPM is converted beside it by default, inside the timed part

@@ -2,7 +2,9 @@
 
 The fp32 kernel follows an explicit arithmetic contract that
 oracle/rt_oracle.cpp's MODE_MIRROR32 restates op for op, so the expected
-result is bit-for-bit equality.  The stated tolerance is the
+result is bit-for-bit equality: with the kernel's default loop-free samplers
+against MODE_MIRROR32 | DIRECT (KERNEL32), with RT_FLAG_REJECTION_SAMPLERS
+(vec3a.clj:74-86's rejection loops) against MODE_MIRROR32.  The stated tolerance is the
 floor the test enforces: >= 99.5 % of pixels within 1e-4 absolute per
 channel and image-mean |diff| <= 1e-5; the bit-exact fraction is asserted
 separately at >= 99.5 %.
@@ -18,7 +20,22 @@ TOL_ABS = 1e-4
 TOL_FRAC = 0.995
 
 
-PRODUCT_VARIANTS = (0, 5, 12, 16, 18, 22, 24, 26)
+PRODUCT_VARIANTS = (0, 5, 12, 16, 18, 22, 24, 26, 28)
+# the fp32 mirrors of the kernel's default contract (loop-free samplers), main and realm semantics
+KERNEL32 = oracle.MODE_MIRROR32 | oracle.DIRECT
+KERNEL_REALM32 = oracle.MODE_REALM32 | oracle.DIRECT
+SAMPLERS = ("direct", "rejection")
+
+
+def _flags(samplers):
+    from rtclj._lib import RT_FLAG_REJECTION_SAMPLERS
+    return RT_FLAG_REJECTION_SAMPLERS if samplers == "rejection" else 0
+
+
+def _mode(samplers, realm=False):
+    """The oracle mode mirroring the kernel with these samplers."""
+    base = oracle.MODE_REALM32 if realm else oracle.MODE_MIRROR32
+    return base | (oracle.DIRECT if samplers == "direct" else 0)
 
 
 class variant:
@@ -45,8 +62,8 @@ def _ref_scene():
     return R.Scene.from_bodies(R.hittables)
 
 
-def _mirror(scene, cam, w, h, spp, depth, seed=1, rows=None, sample_begin=0):
-    out, _, segs, smp = oracle.render(oracle.MODE_MIRROR32, scene.sphere.astype(np.float64), scene.kind,
+def _mirror(scene, cam, w, h, spp, depth, seed=1, rows=None, sample_begin=0, mode=KERNEL32):
+    out, _, segs, smp = oracle.render(mode, scene.sphere.astype(np.float64), scene.kind,
                                       scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
                                       seed=seed, rows=rows, sample_begin=sample_begin)
     return out, segs, smp
@@ -64,26 +81,28 @@ def _assert_parity(gpu, ref, label):
     return exact
 
 
-def test_reference_scene_matches_mirror(gpu_lib):
+@pytest.mark.parametrize("samplers", SAMPLERS)
+def test_reference_scene_matches_mirror(gpu_lib, samplers):
     from rtclj import raytracing as R
     sc = _ref_scene()
     cam = R.camera(400, 225, **R.REFERENCE_CAMERA)
     st = {}
-    gpu = R.render(sc, cam, 400, 225, spp=16, max_depth=50, seed=7, stats=st)
-    ref, segs, smp = _mirror(sc, cam, 400, 225, 16, 50, seed=7)
+    gpu = R.render(sc, cam, 400, 225, spp=16, max_depth=50, seed=7, stats=st, flags=_flags(samplers))
+    ref, segs, smp = _mirror(sc, cam, 400, 225, 16, 50, seed=7, mode=_mode(samplers))
     _assert_parity(gpu, ref, "reference scene 400x225x16")
     assert st["samples"] == smp == 400 * 225 * 16
     assert st["segments"] == segs, (st["segments"], segs)
 
 
-def test_cover_scene_matches_mirror(gpu_lib):
+@pytest.mark.parametrize("samplers", SAMPLERS)
+def test_cover_scene_matches_mirror(gpu_lib, samplers):
     from rtclj import scenes
     from rtclj import raytracing as R
     sc = scenes.cover(11)
     cam = scenes.cover_camera(200, 112)
     st = {}
-    gpu = R.render(sc, cam, 200, 112, spp=8, max_depth=50, seed=3, stats=st)
-    ref, segs, smp = _mirror(sc, cam, 200, 112, 8, 50, seed=3)
+    gpu = R.render(sc, cam, 200, 112, spp=8, max_depth=50, seed=3, stats=st, flags=_flags(samplers))
+    ref, segs, smp = _mirror(sc, cam, 200, 112, 8, 50, seed=3, mode=_mode(samplers))
     _assert_parity(gpu, ref, "cover 200x112x8")
     assert st["segments"] == segs
 
@@ -183,11 +202,12 @@ def test_row_tiles_and_sample_stripes_compose(gpu_lib):
         assert np.array_equal(sharded, full), (nshards, tile)
 
 
-@pytest.mark.parametrize("v", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 19, 22, 24, 26])
-def test_every_variant_is_bit_exact(gpu_lib, v):
+@pytest.mark.parametrize("samplers", SAMPLERS)
+@pytest.mark.parametrize("v", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16, 17, 18, 19, 22, 24, 26, 28])
+def test_every_variant_is_bit_exact(gpu_lib, v, samplers):
     """Kernel variants (product and diagnostic builds: table in LDS / scalar
     cache, simple / grouped / packed scan, BVH traversals, stats builds) all
-    give the mirror's bits."""
+    give the mirror's bits, with either samplers."""
     from rtclj import scenes
     from rtclj import raytracing as R
     sc = scenes.cover(11)
@@ -195,12 +215,12 @@ def test_every_variant_is_bit_exact(gpu_lib, v):
     cam = scenes.cover_camera(w, h)
     with variant(v) as dll:
         st = {}
-        g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st, library=dll)
+        g = R.render(sc, cam, w, h, spp=spp, seed=4, stats=st, library=dll, flags=_flags(samplers))
         if v in (3, 6, 7, 10, 13, 17, 19):
             import ctypes as C
             d = (C.c_uint64 * 32)()
             assert dll.rt_debug_stats(d) == 0 and d[0] > 0 and d[5] > 0
-    ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4)
+    ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4, mode=_mode(samplers))
     assert np.array_equal(g, ref), f"variant {v}"
     assert st["segments"] == segs
 
@@ -255,26 +275,35 @@ def test_bad_material_rejected(gpu_lib):
     assert ei.value.code == -2
 
 
-def test_gpu_matches_committed_mirror_fixture(gpu_lib):
-    """Committed golden vectors (tests/golden/mirror_small.npz): bit-exact."""
+@pytest.mark.parametrize("samplers", SAMPLERS)
+def test_gpu_matches_committed_mirror_fixture(gpu_lib, samplers):
+    """Committed golden vectors, bit-exact: tests/golden/mirror_small_direct.npz
+    (the default samplers) and mirror_small.npz (RT_FLAG_REJECTION_SAMPLERS),
+    main and realm semantics."""
     from pathlib import Path
     from rtclj import raytracing as R
-    from rtclj import scenes
-    f = np.load(Path(__file__).parent / "golden" / "mirror_small.npz")
+    from rtclj import realm, scenes
+    name = "mirror_small_direct.npz" if samplers == "direct" else "mirror_small.npz"
+    f = np.load(Path(__file__).parent / "golden" / name)
+    fl = _flags(samplers)
     st = {}
-    g = R.render(_ref_scene(), R.camera(48, 27, **R.REFERENCE_CAMERA), 48, 27, spp=8, seed=3, stats=st)
+    g = R.render(_ref_scene(), R.camera(48, 27, **R.REFERENCE_CAMERA), 48, 27, spp=8, seed=3, stats=st, flags=fl)
     assert np.array_equal(g, f["reference_48x27_spp8_seed3"]) and st["segments"] == f["segments"][0]
-    g = R.render(scenes.cover(11), scenes.cover_camera(32, 18), 32, 18, spp=4, seed=5, stats=st)
+    g = R.render(scenes.cover(11), scenes.cover_camera(32, 18), 32, 18, spp=4, seed=5, stats=st, flags=fl)
     assert np.array_equal(g, f["cover_32x18_spp4_seed5"]) and st["segments"] == f["segments"][1]
+    g = realm.render(R.Scene.from_bodies(realm.hittables), realm.camera(48, 27), 48, 27, spp=8, max_depth=50,
+                     seed=3, stats=st, flags=fl)
+    assert np.array_equal(g, f["realm_48x27_spp8_seed3"]) and st["segments"] == f["segments"][2]
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_gpu_reproduces_reference_scene_ppm(gpu_lib, seed):
+@pytest.mark.parametrize("seed,samplers", [(1, "direct"), (2, "direct"), (1, "rejection")])
+def test_gpu_reproduces_reference_scene_ppm(gpu_lib, seed, samplers):
     """Full reference config (400x225, 100 spp, depth 50) vs the reference's
-    own scene.ppm, within SURVEY.md §8c's statistical tolerance."""
+    own scene.ppm, within SURVEY.md §8c's statistical tolerance: the default
+    loop-free samplers (two seeds) and the rejection samplers."""
     from rtclj import raytracing as R
     from test_oracle_pinning import within_tolerance
-    rgb = R.main(100, 50, out_path="/tmp/rtclj_scene_gpu.ppm", seed=seed)
+    rgb = R.main(100, 50, out_path="/tmp/rtclj_scene_gpu.ppm", seed=seed, flags=_flags(samplers))
     ok, info = within_tolerance(rgb)
     assert all(ok.values()), (ok, info)
     assert np.array_equal(R.read_ppm("/tmp/rtclj_scene_gpu.ppm"), rgb)
@@ -478,17 +507,19 @@ def test_bvh_large_scene_falls_back(gpu_lib, vsel):
     assert np.array_equal(out[5], out[vsel])
 
 
-def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None):
-    out, _, segs, smp = oracle.render(oracle.MODE_REALM32, scene.sphere.astype(np.float64), scene.kind,
+def _realm_mirror(scene, cam, w, h, spp, depth, seed=1, rows=None, mode=KERNEL_REALM32):
+    out, _, segs, smp = oracle.render(mode, scene.sphere.astype(np.float64), scene.kind,
                                       scene.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, depth,
                                       seed=seed, rows=rows)
     return out, segs, smp
 
 
-@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18, 22, 24, 26])
-def test_realm_flag_matches_mirror(gpu_lib, vsel):
+@pytest.mark.parametrize("samplers", SAMPLERS)
+@pytest.mark.parametrize("vsel", [0, 5, 11, 16, 18, 22, 24, 26, 28])
+def test_realm_flag_matches_mirror(gpu_lib, vsel, samplers):
     """RT_FLAG_REALM (realm.raytracing semantics) through the kernel == the
-    oracle's MODE_REALM32, bit for bit: the realm scene and the cover scene."""
+    oracle's MODE_REALM32 (| DIRECT with the default samplers), bit for bit:
+    the realm scene and the cover scene."""
     from rtclj import raytracing as R
     from rtclj import realm, scenes
     from rtclj._lib import lib
@@ -497,8 +528,9 @@ def test_realm_flag_matches_mirror(gpu_lib, vsel):
     with variant(vsel) as dll:
         for sc, cam, w, h, spp in cases:
             st = {}
-            g = realm.render(sc, cam, w, h, spp=spp, max_depth=50, seed=3, stats=st, library=dll)
-            ref, segs, smp = _realm_mirror(sc, cam, w, h, spp, 50, seed=3)
+            g = realm.render(sc, cam, w, h, spp=spp, max_depth=50, seed=3, stats=st, library=dll,
+                             flags=_flags(samplers))
+            ref, segs, smp = _realm_mirror(sc, cam, w, h, spp, 50, seed=3, mode=_mode(samplers, realm=True))
             assert np.array_equal(g, ref), (vsel, w, h)
             assert st["segments"] == segs and st["samples"] == smp
 
@@ -534,11 +566,13 @@ def test_realm_shards_and_fixture(gpu_lib):
 
 def test_compact_variant_limits(gpu_lib):
     """Variant 22 (the 4-body walk in a compact LDS image: u8 node-index
-    stack, u32 pixel sums, seven workgroups per CU), when selected, runs only
-    where a u32 sum cannot overflow: spp <= 255 and every albedo within
-    [-1, 1]. At spp 255 -- the largest sums -- it equals the mirror bit for
-    bit; at 256, or with an albedo above 1, the launch runs 16 (u64 sums).
-    The default selector runs 22 wherever it applies."""
+    stack, u32 pixel sums with their wraps counted in a byte per channel,
+    seven workgroups per CU), when selected, runs only where those sums
+    cannot overflow: spp < 65536 and every albedo within [-1, 1] (a sample
+    adds at most 2^24 per channel, so a channel wraps at most spp / 256 <
+    256 times). At spp 255 -- the largest sums without a wrap -- it equals
+    the mirror bit for bit; at 65536, or with an albedo above 1, the launch
+    runs 16 (u64 sums). The default selector runs 22 wherever it applies."""
     import ctypes as C
     from rtclj import raytracing as R
     from rtclj import scenes
@@ -560,6 +594,13 @@ def test_compact_variant_limits(gpu_lib):
     assert launch_variant(sc, 3840, 2160, 500) == (22, 7)   # C2 (its sums count their wraps)
     assert launch_variant(sc, 3840, 2160, 1000) == (22, 7)  # C3
     assert launch_variant(sc, 64, 36, 65536)[0] == 16       # a channel could wrap 256 times
+    # a launch of few 8 x 8 tiles (below twice the device's workgroup slots):
+    # 22's image on whole 8 x 4-pixel pools (28) instead of sample splits --
+    # C1's 8- and 4-GPU shards; a small frame too
+    assert launch_variant(sc, 1200, 84, 100) == (28, 7)
+    assert launch_variant(sc, 1200, 168, 100) == (28, 7)
+    assert launch_variant(sc, 1200, 340, 100) == (22, 7)   # (2-GPU shard: 6,375 tiles, whole 8 x 8)
+    assert launch_variant(sc, 200, 112, 100) == (28, 7)
     with variant(22):
         assert launch_variant(sc, 1200, 675, 100) == (22, 7)
         assert launch_variant(sc, 1200, 675, 255)[0] == 22
@@ -578,11 +619,12 @@ def test_compact_variant_limits(gpu_lib):
 
 @pytest.mark.parametrize("scene_kind,w,h,spp", [("sky", 24, 16, 1300), ("cover", 48, 27, 600)])
 def test_compact_variant_counts_wraps(gpu_lib, scene_kind, w, h, spp):
-    """spp > 255 in the compact variant (22): a pixel's u32 sum wraps past
+    """spp > 255 in the compact variant: a pixel's u32 sum wraps past
     2^32 every ~256 bright samples and the wraps are counted per channel
     (trace_kernel.h s_carry). A sky-only frame (colour up to 1: ~4 wraps per
     channel at 1300 spp) and the cover scene at 600 spp equal the mirror bit
-    for bit; both launches run 22."""
+    for bit, on 22 (selected) and on the default for these small frames, 28
+    (the same image on 8 x 4-pixel pools)."""
     import ctypes as C
     from rtclj import raytracing as R
     from rtclj import scenes
@@ -593,21 +635,22 @@ def test_compact_variant_counts_wraps(gpu_lib, scene_kind, w, h, spp):
     else:
         sc = scenes.cover(11)
         cam = scenes.cover_camera(w, h)
-    if True:
-        ds = C.c_void_p()
-        check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
-        try:
-            o = (C.c_int * 4)()
-            p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=50, seed=1)
-            check(lib.rt_launch_occupancy(ds, C.byref(p), o))
-            assert o[3] == 22, o[3]
-        finally:
-            lib.rt_scene_free(ds)
-    st = {}
-    g = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=4, stats=st)
     ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4)
-    assert np.array_equal(g, ref)
-    assert st["segments"] == segs
+    for vsel, want in ((0, 28), (22, 22)):
+        with variant(vsel):
+            ds = C.c_void_p()
+            check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
+            try:
+                o = (C.c_int * 4)()
+                p = rt_params(width=w, height=h, row_begin=0, row_end=h, spp=spp, max_depth=50, seed=1)
+                check(lib.rt_launch_occupancy(ds, C.byref(p), o))
+                assert o[3] == want, (vsel, o[3])
+            finally:
+                lib.rt_scene_free(ds)
+            st = {}
+            g = R.render(sc, cam, w, h, spp=spp, max_depth=50, seed=4, stats=st)
+        assert np.array_equal(g, ref), vsel
+        assert st["segments"] == segs
 
 
 def test_compact_variant_wide_frame(gpu_lib):
@@ -635,6 +678,6 @@ def test_compact_variant_wide_frame(gpu_lib):
     cam = scenes.cover_camera(w, h)
     g = R.render(sc, cam, w, h, spp=1, seed=5)
     cols = (65520, 65600)
-    ref, _, _, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+    ref, _, _, _ = oracle.render(KERNEL32, sc.sphere.astype(np.float64), sc.kind,
                                  sc.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, 1, 50, seed=5, cols=cols)
     assert np.array_equal(g[:, cols[0]:cols[1]], ref[:, cols[0]:cols[1]])

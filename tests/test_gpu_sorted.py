@@ -5,7 +5,7 @@ workgroup's paths to the waves by key before every ray-color level (20:
 fresh samples, then the 8 direction octants; 21: live paths packed only).
 The paths move between lanes through LDS, but each is computed with the same
 fp32 ops, and the pixel sums are integers: every frame must equal the
-oracle's fp32 mirror (MODE_MIRROR32) bit for bit, with the same segment
+oracle's fp32 mirror (MODE_MIRROR32 | DIRECT) bit for bit, with the same segment
 count -- whole tiles, sample splits, interleaved shards, realm semantics,
 ragged tiles, depth 1 and the recorded tile order.
 """
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _mirror(sc, cam, w, h, spp, depth, seed, realm=False, rows=None):
-    mode = oracle.MODE_REALM32 if realm else oracle.MODE_MIRROR32
+    mode = (oracle.MODE_REALM32 if realm else oracle.MODE_MIRROR32) | oracle.DIRECT   # the kernel's default samplers
     out, _, segs, _ = oracle.render(mode, sc.sphere.astype(np.float64), sc.kind, sc.mat.astype(np.float64),
                                     cam.as_list(), cam.defocus, w, h, spp, depth, seed=seed, rows=rows)
     return out, segs

@@ -3,7 +3,7 @@ once every tile has been, join the tiles still running and claim batches of
 their samples from the tile's shared counter until it is spent; a shared
 tile's integer pixel sums meet in a per-tile buffer.  Integer sums do not
 depend on who ran which sample, so every frame must equal the oracle's fp32
-mirror (MODE_MIRROR32) bit for bit, with helpers actually joining
+mirror (MODE_MIRROR32 | DIRECT) bit for bit, with helpers actually joining
 (rt_steal_stats) -- by default, and with the knobs (RTCLJ_STEAL_MIN,
 RTCLJ_THIEVES; read at every launch) at their extremes.
 """
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _mirror(sc, cam, w, h, spp, seed, rows=None):
-    out, _, _, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+    out, _, _, _ = oracle.render(oracle.MODE_MIRROR32 | oracle.DIRECT, sc.sphere.astype(np.float64), sc.kind,
                                  sc.mat.astype(np.float64), cam.as_list(), cam.defocus, w, h, spp, 50,
                                  seed=seed, rows=rows)
     return out

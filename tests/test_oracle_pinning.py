@@ -95,6 +95,20 @@ def test_mirror32_reproduces_scene_ppm_and_tracks_ref64(ref64):
     assert np.abs(lin32 - lin64).mean() < 1e-4
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_direct_sampler_mirror_reproduces_scene_ppm(seed):
+    """The kernel's default contract -- the fp32 mirror with the loop-free
+    samplers (MODE_MIRROR32 | DIRECT; include/rt.h
+    RT_FLAG_REJECTION_SAMPLERS) -- against the reference's own scene.ppm with
+    the same SURVEY.md §8c tolerances (measured: block means 0.136 / 1.18 at
+    seed 1, 0.141 / 2.00 at seed 2; the rejection mirror 0.140 / 1.59,
+    0.150 / 1.67)."""
+    lin, seg = _render(oracle.MODE_MIRROR32 | oracle.DIRECT, seed=seed)
+    ok, info = within_tolerance(_vq(lin))
+    assert all(ok.values()), (ok, info)
+    assert seg == pytest.approx(3.675, abs=0.02)
+
+
 def test_book_metal_variant_is_rejected():
     """Negative control: normalising d before the metal
     reflect (the book's code) must not pass the scene.ppm tolerance."""
@@ -104,18 +118,21 @@ def test_book_metal_variant_is_rejected():
     assert info["block_max"] > 5.0
 
 
-def test_mirror_small_fixture_regression():
+@pytest.mark.parametrize("name,direct", [("mirror_small.npz", 0), ("mirror_small_direct.npz", 0x30)])
+def test_mirror_small_fixture_regression(name, direct):
+    """The committed mirror renders (tests/golden/make_golden.py): with the
+    rejection samplers and with the kernel's default loop-free ones."""
     from rtclj import raytracing as R
     from rtclj import scenes
-    f = np.load(G / "mirror_small.npz")
+    f = np.load(G / name)
     sc = R.Scene.from_bodies(R.hittables)
     cam = R.camera(48, 27, **R.REFERENCE_CAMERA)
-    out, _, segs, _ = oracle.render(oracle.MODE_MIRROR32, sc.sphere.astype(np.float64), sc.kind,
+    out, _, segs, _ = oracle.render(oracle.MODE_MIRROR32 | direct, sc.sphere.astype(np.float64), sc.kind,
                                     sc.mat.astype(np.float64), cam.as_list(), cam.defocus, 48, 27, 8, 50, seed=3)
     assert np.array_equal(out, f["reference_48x27_spp8_seed3"]) and segs == f["segments"][0]
     cs = scenes.cover(11)
     cc = scenes.cover_camera(32, 18)
-    out, _, segs, _ = oracle.render(oracle.MODE_MIRROR32, cs.sphere.astype(np.float64), cs.kind,
+    out, _, segs, _ = oracle.render(oracle.MODE_MIRROR32 | direct, cs.sphere.astype(np.float64), cs.kind,
                                     cs.mat.astype(np.float64), cc.as_list(), cc.defocus, 32, 18, 4, 50, seed=5)
     assert np.array_equal(out, f["cover_32x18_spp4_seed5"]) and segs == f["segments"][1]
 

@@ -67,6 +67,8 @@ def test_ppm_to_png_accepts_any_whitespace_and_a_lower_max_value(R, tmp_path):
     ("P3\n2 1\n255\n0 0 0\n1 1\n", -1),   # truncated pixel data
     ("P3\n1 1\n9\n10 0 0\n", -1),         # value above the maximum
     ("P3\n1 1\n255\n0 x 0\n", -1),        # not a number
+    ("P3\n1 1\n255\n0 0 99999999999999999999999\n", -1),   # a 23-digit token (stops at the tenth digit)
+    ("P3\n1234567890 1\n255\n0 0 0\n", -1),                # a 10-digit dimension
 ])
 def test_ppm_to_png_rejects_malformed_input(R, tmp_path, text, code):
     from rtclj import RTError

@@ -80,9 +80,10 @@ def test_main_semantics_fail_the_realm_fixture():
     assert not checks["block_max"] and not checks["block_mean"], checks
 
 
-def test_realm_mirror_matches_committed_fixture():
-    fx = np.load(G / "mirror_small.npz")
-    lin, segs, _ = _render(oracle.MODE_REALM32, spp=8, seed=3, w=48, h=27)
+@pytest.mark.parametrize("name,direct", [("mirror_small.npz", 0), ("mirror_small_direct.npz", 0x30)])
+def test_realm_mirror_matches_committed_fixture(name, direct):
+    fx = np.load(G / name)
+    lin, segs, _ = _render(oracle.MODE_REALM32 | direct, spp=8, seed=3, w=48, h=27)
     assert np.array_equal(lin, fx["realm_48x27_spp8_seed3"])
     assert segs == int(fx["segments"][2])
 
