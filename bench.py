@@ -267,7 +267,9 @@ def stats_leg(scene, cam, p, device, out_numel):
                              "random_unit_trips": dbg[14] / wi, "disk_trips": dbg[15] / wi,
                              "dielectric_blocks": dbg[19] / wi, "dielectric_lanes": dbg[20] / max(dbg[19], 1),
                              "lambert_metal_blocks": dbg[21] / wi,
-                             "lambert_metal_lanes": dbg[22] / max(dbg[21], 1)}}
+                             "lambert_metal_lanes": dbg[22] / max(dbg[21], 1),
+                             "sums_blocks": dbg[23] / wi, "refills": dbg[24] / wi, "claims": dbg[25] / wi,
+                             "drain_checks": dbg[26] / wi}}
     if v != 5:
         res.update({"nodes": dbg[2] / segs, "leaf_pairs": pairs_per_leaf * dbg[3] / segs,
                     "exact_tests": dbg[4] / segs})
@@ -637,27 +639,32 @@ def main():
     # a new shape's first launch (no tile costs yet: tiles in plain dispatch
     # order, as a process's first frame runs), timed once the GPU is warm:
     # after a launch of another shape (8 rows fewer), which makes this frame's
-    # shape new again; the second such pair is reported.  plain_ms: the same
-    # with the schedule off (rt_set_schedule(1)), for comparison
+    # shape new again.  Alternated with the same with the schedule off
+    # (rt_set_schedule(1)), also after another shape's launch, 5 pairs; the
+    # medians are reported (single launches move by +-0.1 ms)
     first_ms = plain_ms = None
+    first_all, plain_all = [], []
     if a.warmup > 0 and a.schedule == 0 and p.row_end - p.row_begin > 16:
         other = type(p).from_buffer_copy(p)
         other.row_end = p.row_end - 8
-        for _ in range(2):
+
+        def new_shape_launch(sched):
+            check(lib.rt_set_schedule(sched))
             step(0, other)
+            torch.cuda.synchronize()
             g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             g0.record(stream)
             step(0, p)
             g1.record(stream)
             torch.cuda.synchronize()
-            first_ms = g0.elapsed_time(g1)
-        check(lib.rt_set_schedule(1))
-        step(0, p)
-        g0.record(stream)
-        step(0, p)
-        g1.record(stream)
-        torch.cuda.synchronize()
-        plain_ms = g0.elapsed_time(g1)
+            return g0.elapsed_time(g1)
+
+        new_shape_launch(a.schedule)   # (untimed: the first pair's launches)
+        for r in range(5):
+            for sched in ((a.schedule, 1) if r % 2 == 0 else (1, a.schedule)):
+                (first_all if sched == a.schedule else plain_all).append(new_shape_launch(sched))
+        first_ms = statistics.median(first_all)
+        plain_ms = statistics.median(plain_all)
         check(lib.rt_set_schedule(a.schedule))
         step(0, p)   # (the record again, for the timed steps)
 
@@ -702,6 +709,7 @@ def main():
             "launch_span_ms_avg": sum(kern_ms) / len(kern_ms),
             "kernel_ms_max": max(kern_ms), "rows": rows, "segments": main_t["segments"],
             "samples": main_t["samples"], "first_launch_ms": first_ms, "plain_ms": plain_ms,
+            "first_launch_all": first_all, "plain_all": plain_all,
             "ms_per_frame": main_t["elapsed_s"] / a.steps * 1e3,
             "other_elapsed_s": other_t["elapsed_s"] if other_t else None,
             "other_samples": other_t["samples"] if other_t else None}
@@ -806,11 +814,15 @@ def main():
             "kernel_ms_avg": kern_avg_ms, "launch_span_ms_max": mine["kernel_ms_max"],
             "dispatch_order": {"kernel_ms": mine["first_launch_ms"],
                                "plain_schedule_off_ms": mine["plain_ms"],
+                               "kernel_ms_all": mine["first_launch_all"],
+                               "plain_schedule_off_ms_all": mine["plain_all"],
                                "note": "the first launch of a new shape (no tile costs yet: tiles in plain dispatch "
                                        "order, as a process's first frame runs), timed after the GPU is warm, right "
                                        "after a launch of another shape; plain_schedule_off_ms: the same frame with "
-                                       "the schedule off (rt_set_schedule(1)); the timed steps dispatch longest first by "
-                                       "the previous launches' per-tile durations (each added to half the record before it)"},
+                                       "the schedule off (rt_set_schedule(1)), also a new shape; medians of 5 "
+                                       "alternated pairs (events around the whole rt_launch: its fills and kernels); "
+                                       "the timed steps dispatch longest first by the previous launches' per-tile "
+                                       "durations (each added to half the record before it)"},
             "scaling_basis": summary["scaling_basis"], "single_frame": summary["single_frame"],
             "pipelined": summary["pipelined"],
             "frames_in_flight": {"streams": inflight, "rt_launch_flags": "RT_FLAG_STREAMED" if inflight > 1 else 0,

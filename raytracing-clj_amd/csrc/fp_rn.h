@@ -5,6 +5,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// (block markers of the ISA listing, trace_kernel.h; here for the rare branches)
+#ifndef RT_MARK
+#ifdef RTCLJ_ISA_MARKS
+#define RT_MARK(name) asm volatile(";@@ " name)
+#else
+#define RT_MARK(name) ((void)0)
+#endif
+#endif
+
 namespace rtclj {
 
 // Correctly rounded sqrt, the same bits as sqrtf for every input: for
@@ -23,7 +32,10 @@ __device__ __forceinline__ float sqrt_rn_normal(float x) {
   return r;
 }
 __device__ __forceinline__ float sqrt_rn(float x) {
-  if (__builtin_expect(!(x >= 0x1p-96f), 0)) return sqrtf(x);
+  if (__builtin_expect(!(x >= 0x1p-96f), 0)) {
+    RT_MARK("cold");
+    return sqrtf(x);
+  }
   return sqrt_rn_normal(x);
 }
 
@@ -41,7 +53,10 @@ __device__ __forceinline__ float rcp_rn_normal(float b) {
 // reciprocal is subnormal, negatives, inf, NaN) through the division itself,
 // a branch the kernel's inputs do not take.
 __device__ __forceinline__ float rcp_rn(float b) {
-  if (__builtin_expect(!(b >= 0x1p-126f && b < 0x1p126f), 0)) return 1.0f / b;
+  if (__builtin_expect(!(b >= 0x1p-126f && b < 0x1p126f), 0)) {
+    RT_MARK("cold");
+    return 1.0f / b;
+  }
   return rcp_rn_normal(b);
 }
 

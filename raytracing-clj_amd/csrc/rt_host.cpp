@@ -280,7 +280,9 @@ struct Ctx {
   // (take_ctx), with the tile orders recorded so far.
   bool null_stream = false;
   hipStream_t stream = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  // e0 .. e1 the kernel, eg .. e2 the D2H (eg right behind e1 when the copy
+  // is enqueued with the launch, else where finish_shard enqueues it)
+  hipEvent_t e0 = nullptr, e1 = nullptr, eg = nullptr, e2 = nullptr;
   float* d_out = nullptr;
   size_t d_cap = 0;           // floats
   uint8_t* d_u8 = nullptr;    // rt_render_u8's bytes
@@ -301,6 +303,7 @@ struct Ctx {
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
+    if (eg) (void)hipEventDestroy(eg);
     if (e2) (void)hipEventDestroy(e2);
     if (d_out) (void)hipFree(d_out);
     if (d_u8) (void)hipFree(d_u8);
@@ -580,6 +583,7 @@ void start_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb
   if (e == hipSuccess && !cx->stream && !cx->null_stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && !cx->e0) e = hipEventCreate(&cx->e0);
   if (e == hipSuccess && !cx->e1) e = hipEventCreate(&cx->e1);
+  if (e == hipSuccess && !cx->eg) e = hipEventCreate(&cx->eg);
   if (e == hipSuccess && !cx->e2) e = hipEventCreate(&cx->e2);
   if (e == hipSuccess && !cx->d_cnt) e = hipMalloc(&cx->d_cnt, 2 * sizeof(uint64_t));
   if (e == hipSuccess && !cx->h_cnt) e = hipHostMalloc(&cx->h_cnt, 2 * sizeof(uint64_t), hipHostMallocDefault);
@@ -624,7 +628,9 @@ void start_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb
     return;
   }
   e = hipEventRecord(cx->e1, cx->stream);
-  // (u8: the quantiser's few microseconds fall in d2h_ms)
+  // (u8: the quantiser's few microseconds fall in d2h_ms when the copy
+  // follows at once)
+  if (e == hipSuccess && gather_now) e = hipEventRecord(cx->eg, cx->stream);
   if (e == hipSuccess && u8 && nfl) e = static_cast<hipError_t>(quantize_launch(cx->d_out, cx->d_u8, nfl, cx->stream));
   if (e == hipSuccess && gather_now) {
     e = enqueue_gather(sh, out_rgb, u8, rows_total, ntiles, nshards, shard_idx);
@@ -643,12 +649,15 @@ void finish_shard(Shard* sh, void* out_rgb, bool u8, int rows_total, int ntiles,
     const auto t_wait = Clock::now();
     hipError_t e = hipSetDevice(sh->device);
     if (e == hipSuccess && !sh->gathered) e = hipStreamSynchronize(cx->stream);
+    // (a submitted frame's copy starts now: d2h_ms times it from here, not
+    // from the kernel's end, which the caller's rt_render_wait may be long after)
+    if (e == hipSuccess && !sh->gathered) e = hipEventRecord(cx->eg, cx->stream);
     if (e == hipSuccess && !sh->gathered) e = enqueue_gather(sh, out_rgb, u8, rows_total, ntiles, nshards, shard_idx);
     if (e == hipSuccess) e = hipStreamSynchronize(cx->stream);
     sh->wait_ms = ms_since(t_wait);
     float d2h = 0.0f;
     if (e == hipSuccess) e = hipEventElapsedTime(&sh->ms, cx->e0, cx->e1);
-    if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->e1, cx->e2);
+    if (e == hipSuccess) e = hipEventElapsedTime(&d2h, cx->eg, cx->e2);
     sh->d2h_ms = d2h;
     if (e != hipSuccess) {
       sh->status = RT_E_HIP;

@@ -90,6 +90,28 @@ __global__ __launch_bounds__(256) void fill_kernel(uint32_t* __restrict__ p, uin
   for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) p[i] = v;
 }
 
+// Several fills in one launch: the zeroings a launch of a new shape needs
+// (its tile-cost record, the sharing words and owner table) as one kernel in
+// front of the trace kernel instead of one small launch each.
+struct FillSet {
+  static constexpr int kMax = 6;
+  uint32_t* p[kMax];
+  uint32_t v[kMax];
+  size_t n[kMax];
+  int count = 0;
+  void add(void* ptr, int byte_value, size_t bytes) {
+    p[count] = static_cast<uint32_t*>(ptr);
+    v[count] = static_cast<uint32_t>(byte_value & 0xff) * 0x01010101u;
+    n[count] = bytes / 4;
+    ++count;
+  }
+};
+__global__ __launch_bounds__(256) void fill_set_kernel(const FillSet f) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+  for (int k = 0; k < f.count; ++k)
+    for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; i < f.n[k]; i += stride) f.p[k][i] = f.v[k];
+}
+
 // rt_quantize on the device (rt_render_u8, rt_quantize_device): a channel's
 // byte is the number of thresholds t[1..255] <= it (rt_internal.h), found by
 // an 8-step binary search in LDS -- NaN fails every compare and gets 0, as
@@ -196,8 +218,9 @@ __global__ __launch_bounds__(1024) void plan_kernel(const unsigned* __restrict__
 //      waves, 64 VGPRs: 8 waves per SIMD): the default for scenes whose
 //      4-body image is too big for 22 (C4), where 22 applies and two fit a CU
 //   24 the same in 8-wave workgroups: where three of those fit and not two of 26's
-//   28 22 on 8 x 4-pixel pools: the default for a launch of 22 with fewer 8 x 8
-//      tiles than twice the workgroups the device holds (a multi-GPU shard)
+//   28 22 on 8 x 4-pixel pools (whole pools for launches of few 8 x 8 tiles
+//      instead of sample splits: measured slower, selected only explicitly
+//      or by RTCLJ_TH4)
 //   18 BVH in LDS, 8-body leaves (large scenes where 24 does not fit)
 //   12 BVH (2-body leaves) read from global memory: a tree too big for LDS
 //    5 linear scan, grouped, table through the scalar cache: a tree too deep
@@ -226,9 +249,8 @@ static const Variant& variant_table(int v) {
   // (and in 16-wave workgroups, 64 VGPRs: 8 waves per SIMD)
   // (trace_w16.hip, compiled with its own scheduler flag)
   static const Variant v26{trace_kernel_w16(), true, false, SCAN_BVHQ7, 1024};
-  // (22 on 8 x 4-pixel pools: launches of few 8 x 8 tiles -- a shard of a
-  // multi-GPU frame -- run whole pools of half the pixels instead of sample
-  // splits)
+  // (22 on 8 x 4-pixel pools: whole pools of half the pixels for launches of
+  // few 8 x 8 tiles instead of sample splits; measured slower)
   static const Variant v28{RT_KWT(SRC_LDS, SCAN_BVHQ7, false, 4, 4), true, false, SCAN_BVHQ7, 256, 4};
   switch (v) {
     case 0: return placeholder;
@@ -301,6 +323,14 @@ struct Schedule {
   int* order = nullptr;
   int cap = 0;          // tiles the buffers hold
   bool ready = false;   // order[] holds a permutation of key's tiles (stream-ordered)
+  // The sort of the last launch's record (order_kernel, and plan_kernel for a
+  // planned split) is enqueued at the start of the next launch of the shape
+  // on the stream, not behind the trace kernel: a frame's launch ends with
+  // its trace kernel (a one-frame process never pays the sort), and a frame
+  // loop pays it once per frame as before.  sort_plan: the plan's unit count
+  // (-1: no plan).
+  bool sort_pending = false;
+  int sort_plan = -1;
   ScheduleKey key{};
   unsigned long long* part = nullptr;   // [rows][width][3] pixel sums of split tiles (zero between launches)
   size_t part_cap = 0;                  // u64 elements
@@ -699,14 +729,17 @@ static int launch_variant(const rt_dscene& ds, const rt_params& p) {
       vsel = 24;
   }
   if ((vsel == 24 || vsel == 26 || vsel == 28) && !compact_ok(ds, p)) vsel = 16;
-  // A launch of 22 with few 8 x 8 tiles -- fewer than kWholeTh4 (RTCLJ_TH4,
-  // default 2; 0: never) x the workgroups the device holds, a shard of a
+  // RTCLJ_TH4=r (A/B knob, default 0 = never): a launch of 22 with fewer
+  // 8 x 8 tiles than r x the workgroups the device holds -- a shard of a
   // multi-GPU frame -- runs 28: the same image on 8 x 4-pixel pools, whole,
-  // where 22 would split every tile's samples over 2-3 workgroups (each
-  // split re-loads the tree, drains its own pool and adds its sums through
-  // HBM atomics and finalize_kernel).  DESIGN.md §6.
+  // where 22 splits every tile's samples over 2-3 workgroups.  Measured at r
+  // = 2 (profiles/r06/th4/): C1's 8-rank shard 1.62 ms against 0.84 with the
+  // splits, the 4-rank 1.56 against 1.37 (the whole 8 x 4 pools are 1.84
+  // rounds of 3,200-sample units: the last round's long units are the tail),
+  // and 28 costs 5 % more per sample on the whole C1 frame (4.95 vs 4.71 ms:
+  // a pool of half the pixels drains twice as often).  DESIGN.md §6.
   if (sel == 0 && vsel == 22) {
-    const int ratio = env_int("RTCLJ_TH4", 2, 0);
+    const int ratio = env_int("RTCLJ_TH4", 0, 0);
     if (ratio > 0) {
       const int rows = rows_out(p);
       const int64_t n8 = static_cast<int64_t>((p.width + kTile - 1) / kTile) * ((rows + kTile - 1) / kTile);
@@ -998,10 +1031,13 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     key.gy = gy;
     if (std::memcmp(&sch->key, &key, sizeof key) != 0) {
       sch->ready = false;
+      sch->sort_pending = false;   // (that record was another shape's)
       sch->key = key;
       new_shape = true;
     }
   }
+  // the fills this launch needs before its trace kernel, as one launch
+  FillSet fills;
   if (sch && g_schedule.load() == 0) {
     if (sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
       HIP_TRY(hipStreamSynchronize(stream));
@@ -1011,9 +1047,28 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       sch->order = nullptr;
       sch->cap = 0;
       sch->ready = false;
+      sch->sort_pending = false;
       HIP_TRY(hipMalloc(&sch->cost, n_tiles * sizeof(unsigned)));
       HIP_TRY(hipMalloc(&sch->order, n_tiles * sizeof(int)));
       sch->cap = n_tiles;
+    }
+    if (sch->sort_pending) {   // the previous launch's record, sorted now (stream-ordered after it)
+      unsigned* cost = sch->cost;
+      int* order = sch->order;
+      int n = n_tiles;
+      void* sargs[] = {&cost, &order, &n};
+      HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
+      sch->ready = true;
+      sch->sort_pending = false;
+      sch->plan_units = -1;
+      if (sch->sort_plan > 0 && sch->units_cap >= sch->sort_plan) {
+        // the next split launch's cost-balanced units, from this record
+        int2* units = sch->units;
+        int Uk = sch->sort_plan, smax = std::min(p->spp, kSplitMax);
+        void* pargs[] = {&cost, &order, &n, &Uk, &smax, &units};
+        HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&plan_kernel), dim3(1), dim3(1024), pargs, 0, stream));
+        sch->plan_units = sch->sort_plan;
+      }
     }
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
@@ -1027,7 +1082,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       a.unit_tab = sch->units;
     // the costs decay (order_kernel halves them after sorting): zeroed only
     // when this launch shape starts a new history
-    if (!sch->ready) HIP_TRY(static_cast<hipError_t>(fill_async(sch->cost, 0, n_tiles * sizeof(unsigned), stream)));
+    if (!sch->ready) fills.add(sch->cost, 0, n_tiles * sizeof(unsigned));
   }
   // the grid: the units, then (stealing) the thieves, dispatched last, i.e.
   // as the units' slots free up in the launch's tail
@@ -1093,8 +1148,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // epochs, but tile indices of another shape may exceed this one's; a word
     // last published 65,535 launches ago carries the epoch a wrap reuses.)
     if (new_shape) {
-      HIP_TRY(static_cast<hipError_t>(fill_async(sch->owner, 0xff, n_owner * sizeof(int), stream)));
-      HIP_TRY(static_cast<hipError_t>(fill_async(sch->word, 0, n_tiles * sizeof(unsigned long long), stream)));
+      fills.add(sch->owner, 0xff, n_owner * sizeof(int));
+      fills.add(sch->word, 0, n_tiles * sizeof(unsigned long long));
     }
     // owners publish only in the launch's last RTCLJ_SHARE_ROUNDS rounds of
     // units (default 2; a round = the workgroups the device holds at once.
@@ -1123,6 +1178,14 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // batches were round 3's: C1 5.960 -> 5.916 ms, C2 287.9 -> 286.1 ms,
   // profiles/r04/lds_batch/)
   a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 256, 64));
+  if (fills.count) {
+    size_t most = 0;
+    for (int k = 0; k < fills.count; ++k) most = std::max(most, fills.n[k]);
+    const size_t blocks = std::max<size_t>(1, std::min<size_t>((most + 255) / 256, 2048));
+    void* fa[] = {&fills};
+    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&fill_set_kernel), dim3(static_cast<unsigned>(blocks)),
+                            dim3(256), fa, 0, stream));
+  }
   void* args[] = {&a};
   if (split > 1) sch->part_dirty = true;   // (cleared once finalize_kernel is enqueued)
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
@@ -1137,15 +1200,11 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     sch->part_dirty = false;
   }
   if (a.tile_cost) {
-    // the next launch's order, stream-ordered after this kernel (no host sync)
-    unsigned* cost = sch->cost;
-    int* order = sch->order;
-    int n = n_tiles;
-    void* sargs[] = {&cost, &order, &n};
-    HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
-    sch->ready = true;
+    // this record's sort, at the next launch of the shape on the stream
+    sch->sort_pending = true;
+    sch->ready = false;
+    sch->sort_plan = -1;
     if (split > 1 && n_whole == 0 && env_int("RTCLJ_SPLIT_PLAN", 0, 0) != 0) {
-      // the next split launch's cost-balanced units, from this record
       const int U = n_units;
       if (sch->units_cap < U) {   // grow: this stream's kernels may still read the old plan
         HIP_TRY(hipStreamSynchronize(stream));
@@ -1155,13 +1214,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
         HIP_TRY(hipMalloc(&sch->units, U * sizeof(int2)));
         sch->units_cap = U;
       }
-      int2* units = sch->units;
-      int Uk = U, smax = std::min(p->spp, kSplitMax);
-      void* pargs[] = {&cost, &order, &n, &Uk, &smax, &units};
-      HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&plan_kernel), dim3(1), dim3(1024), pargs, 0, stream));
-      sch->plan_units = U;
-    } else {
-      sch->plan_units = -1;
+      sch->sort_plan = U;
     }
   }
   HIP_TRY(hipGetLastError());

@@ -171,6 +171,11 @@ __device__ __forceinline__ float rng_sym(uint32_t& s) {
   return fmaf(static_cast<float>(s >> 8), 0x1p-23f, -1.0f);
 }
 
+// ISA block markers: in a listing built with -DRTCLJ_ISA_MARKS (make isa-marks,
+// tools/isa_blocks.py) each names the block of the kernel the lines after it
+// belong to ("cold": a rare branch); the shipped and diagnostic builds contain
+// none.  (Defined in fp_rn.h, included above.)
+
 // stats builds: count one event per wave (by its first active lane)
 __device__ __forceinline__ void wave_event(uint64_t& c) {
   const uint64_t ex = __builtin_amdgcn_read_exec();
@@ -497,6 +502,9 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   uint64_t st_fresh = 0, st_fresh_lanes = 0;  // wave-level camera-sample blocks, lanes in them
   uint64_t st_diel = 0, st_diel_lanes = 0;    // wave-level dielectric blocks, lanes in them
   uint64_t st_lm = 0, st_lm_lanes = 0;        // wave-level lambertian/metal blocks, lanes in them
+  // wave-level events of the loop's bookkeeping: colour sums
+  // added, refills, batch claims, drain-phase checks (batches spent)
+  uint64_t st_sums = 0, st_refill = 0, st_claim = 0, st_drain = 0;
   uint64_t st_c_cam = 0, st_c_scan = 0, st_c_shade = 0, st_c_acc = 0, st_ts = 0;  // clock split
   uint64_t st_t0 = 0;
   if (STATS || a.tile_cost || a.dbgw) st_t0 = __builtin_amdgcn_s_memrealtime();
@@ -792,6 +800,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // finds every sibling gone -- it takes what is left, keeps its own paths,
   // and counts itself back in.
   auto compact_step = [&]() {
+    RT_MARK("compact_step");
     // (the wave index in an SGPR here: its slots' addresses rebuilt in this
     // cold step, not held in a VGPR -- at 72 VGPRs one was spilled to scratch)
     const int wu = static_cast<int>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
@@ -903,7 +912,9 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         st_lanes += __popcll(ex);
       }
     }
+    RT_MARK("iteration");
     if (kCompact ? j >= 0 : fresh) {
+      RT_MARK("camera");
       if constexpr (STATS) {
         const uint64_t ex = __builtin_amdgcn_read_exec();
         if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -950,7 +961,9 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         float qx, qy2;
         if (a.sampler & RT_SAMPLER_DISK) {
           disk_direct<STATS>(st, qx, qy2, &st_disk, &st_fl);
+          RT_MARK("camera");
         } else {
+          RT_MARK("rejection_disk");
           do {
             if constexpr (STATS) {
               wave_event(st_disk);
@@ -987,6 +1000,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       st_ts = t;
     }
     // ---- one ray-color level: hit-anything over all bodies ----
+    RT_MARK("setup");
     --rem;
     ++segs;
     // |d| and 1/|d| (vec3a/unit as d * (1/|d|)), both correctly rounded; one
@@ -998,6 +1012,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       len = sqrt_rn_normal(len2);
       il = rcp_rn_normal(len);
     } else {
+      RT_MARK("cold");
       len = sqrt_rn(len2);
       il = rcp_rn(len);
     }
@@ -1104,6 +1119,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       // (the 4-body tree in LDS: p is a leaf record's LDS address, see the copy)
       constexpr bool kLeafRec = SRC == SRC_LDS && is_q(SCAN);
       auto leaf = [&](int p) {
+        RT_MARK("leaf");
         if constexpr (STATS) {
           ++st_blk;
           const uint64_t ex = __builtin_amdgcn_read_exec();
@@ -1144,6 +1160,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
           const unsigned b23 = __builtin_amdgcn_perm(nc[3], nc[2], 0x0b090c0cu);
           unsigned m = __builtin_amdgcn_bitop3_b32(b01, b23, 0x01010101u, 0xa8);
           while (m) {
+            RT_MARK("exact");
             if constexpr (STATS) {
               const uint64_t ex = __builtin_amdgcn_read_exec();
               if (lane == __ffsll(static_cast<long long>(ex)) - 1) ++st_consw;
@@ -1155,6 +1172,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
             const int sidx = *(const int __attribute__((address_space(3)))*)(uintptr_t)(pa + 64u + (k >> 1));
             consider_tie(h, disc, sidx);
           }
+          RT_MARK("node");
           return;
         }
 #pragma unroll
@@ -1304,12 +1322,14 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       };
       // the big bodies' leaves first: every lane, so a wave-uniform loop (their
       // hits, e.g. the ground, then cull the tree)
+      RT_MARK("bigleaf");
       for (int b = 0; b < a.n_big_leaves; ++b) {
         if constexpr (kLeafRec)
           leaf(static_cast<int>(lds_addr(nodes)) + a.bvh_off_pairs + ((a.big_pair0 >> 1) + b) * kLeafRecBytes);
         else
           leaf(a.big_pair0 + b * leaf_pairs(SCAN));
       }
+      RT_MARK("tree_setup");
       // the root: the 4-body tree's refs are LDS addresses (relocated as copied)
       int node = SRC == SRC_LDS && SCAN == SCAN_BVHQ ? static_cast<int>(lds_addr(nodes)) : 0;   // (BVHQ7: index 0)
       // the stack top as a pointer into the [entry][lane] stack: one add per
@@ -1322,6 +1342,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       asm volatile("" : "+v"(row_b));
       bool go = true;
       while (go) {
+        RT_MARK("node");
         if constexpr (STATS) {
           ++st_sph;
           const uint64_t ex = __builtin_amdgcn_read_exec();
@@ -1362,6 +1383,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       // the ray's origin and unit direction again from the packed copies the
       // walk used (the same values): the scalar ones are dead through it,
       // six VGPRs fewer at its peak
+      RT_MARK("hit");
       ox = o_xy.x;
       oy = o_xy.y;
       oz = o_zux.x;
@@ -1450,6 +1472,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       oz = hz;
       last = best;
       if (kind == RT_LAMBERTIAN || kind == RT_METAL) {
+        RT_MARK("lambert_metal");
         if constexpr (STATS) {
           const uint64_t ex = __builtin_amdgcn_read_exec();
           if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -1461,10 +1484,13 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         // the segment for these lanes): a wave loops the rejection sampler
         // once for both kinds
         float qx, qy, qz;
-        if (a.sampler & RT_SAMPLER_SPHERE)
+        if (a.sampler & RT_SAMPLER_SPHERE) {
           sphere_direct<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
-        else
+          RT_MARK("lambert_metal");
+        } else {
+          RT_MARK("rejection_sphere");
           random_unit<STATS>(st, qx, qy, qz, &st_ball, &st_fl);
+        }
         if constexpr (STATS) st_fl += kind == RT_LAMBERTIAN ? 6 : 26;
         if (kind == RT_LAMBERTIAN) {
           // material.clj:13-19 + vec3a/near-zero? (vec3a.clj:88-92)
@@ -1501,6 +1527,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         done = true;  // no ::scatter-fn -> black (raytracing.clj:49-54)
       } else {
         // material.clj:34-46 dielectric, reflectance :30-32, refract vec3a.clj:97-101
+        RT_MARK("dielectric");
         if constexpr (STATS) {
           const uint64_t ex = __builtin_amdgcn_read_exec();
           if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -1546,8 +1573,10 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       st_c_shade += t - st_ts;
       st_ts = t;
     }
+    RT_MARK("sums");
     if (done) {   // the sample's colour into its pixel's fixed-point sum (order-free)
       if constexpr (STATS) st_fl += 3;
+      if constexpr (STATS) wave_event(st_sums);
       AccT* acc = &s_acc[q * 3];
       if (kCompactPx && sgpr(kargs_opaque()->spp) > 255) {
         // the u32 sums with their wraps counted (s_carry above)
@@ -1557,6 +1586,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         const uint32_t o2 = __hip_atomic_fetch_add(acc + 2, f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const bool w0 = o0 + f0 < o0, w1 = o1 + f1 < o1, w2 = o2 + f2 < o2;
         if (w0 | w1 | w2) {
+          RT_MARK("cold");
           const int c = q * 3;
           if (w0) atomicAdd(&s_carry[c >> 2], 1u << (8 * (c & 3)));
           if (w1) atomicAdd(&s_carry[(c + 1) >> 2], 1u << (8 * ((c + 1) & 3)));
@@ -1569,8 +1599,10 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       }
     }
     // refill: the lanes whose paths ended take their next indices
+    RT_MARK("refill");
     const uint64_t m = __ballot(done);
     if (m) {
+      if constexpr (STATS) wave_event(st_refill);
       // the lanes in m take the next indices of the wave's batch, in rank
       // order; when it runs out the wave claims another: 64 indices from
       // s_pool_next, or for a shared tile 128-1024 from the tile's word
@@ -1587,6 +1619,8 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         wb += take;
         r0 += take;
         if (r0 >= need || we >= pool) break;
+        RT_MARK("claim");
+        if constexpr (STATS) wave_event(st_claim);
         int g = 0;
         // a shared tile's claims shrink as its pool is spent (guided: an
         // eighth of what is left past this wave's last batch, kShareBatch ..
@@ -1612,6 +1646,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
         we = min(g + want, pool);
         if (wb >= pool) we = pool;   // spent: the lanes left over retire
       }
+      RT_MARK("refill");
       if (done) {
         j = kCompact && nj < 0 ? -2 : nj;
         fresh = true;
@@ -1619,11 +1654,14 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       }
     }
     if constexpr (STATS) st_c_acc += stamp() - st_ts;
+    RT_MARK("compaction");
     if constexpr (kCompact) {
       // spent: out to the compaction step when this wave may post its few
       // paths, or its idle lanes may take posted ones
       // (the limit and the flags from LDS: no registers held for them)
       if (wb >= pool) {
+        RT_MARK("drain_check");
+        if constexpr (STATS) wave_event(st_drain);
         const int lim = sgpr(lds_load(&s_mb_lim[threadIdx.x >> 6]));
         if (lim >= 0) {
           const int left = static_cast<int>(__popcll(__ballot(j >= -1)));
@@ -1637,6 +1675,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
     }
   };
   for (;;) {
+    RT_MARK("loop");
     if constexpr (kCompact) {
       while (j >= -1) iteration();
     } else {
@@ -1655,6 +1694,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
     }
   }
 
+  RT_MARK("epilogue");
   // ---- per-pixel mean (compute-pixel's accum / spp, raytracing.clj:155) ----
   // thread t < 3 * npx writes channel t % 3 of pool pixel t / 3: a tile row's
   // 8 pixels are 24 consecutive floats
@@ -1751,6 +1791,12 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
     if (a.dbg && st_fresh) {
       atomicAdd(&a.dbg[16], static_cast<unsigned long long>(st_fresh));
       atomicAdd(&a.dbg[17], static_cast<unsigned long long>(st_fresh_lanes));
+    }
+    if (a.dbg && (st_sums | st_refill | st_claim | st_drain)) {
+      atomicAdd(&a.dbg[23], static_cast<unsigned long long>(st_sums));
+      atomicAdd(&a.dbg[24], static_cast<unsigned long long>(st_refill));
+      atomicAdd(&a.dbg[25], static_cast<unsigned long long>(st_claim));
+      atomicAdd(&a.dbg[26], static_cast<unsigned long long>(st_drain));
     }
     if (a.dbg && st_blk) {
       atomicAdd(&a.dbg[3], static_cast<unsigned long long>(st_blk));

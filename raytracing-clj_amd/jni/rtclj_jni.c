@@ -29,6 +29,7 @@
  * :172-175) and ppm2png/ppm->png (src/ppm2png.clj:35-87).
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -58,6 +59,56 @@ typedef struct {
   uint8_t* buf;
   size_t len;
 } JFrame;
+
+/* The handles the JVM holds are ids of live frames in this table, never
+ * pointers: waitBytes takes its frame out of the table, so a second wait on
+ * the same handle -- or any number it was never given -- is an argument
+ * error (RuntimeException), not a use-after-free.  Ids are never reused. */
+typedef struct {
+  jlong id;
+  JFrame* jf;
+} FrameSlot;
+static pthread_mutex_t g_frames_mu = PTHREAD_MUTEX_INITIALIZER;
+static FrameSlot* g_frames = NULL;
+static size_t g_nframes = 0, g_capframes = 0;
+static jlong g_next_id = 1;
+
+/* the frame's new handle, 0 when the table cannot grow */
+static jlong frame_register(JFrame* jf) {
+  jlong id = 0;
+  pthread_mutex_lock(&g_frames_mu);
+  if (g_nframes == g_capframes) {
+    const size_t cap = g_capframes ? 2 * g_capframes : 16;
+    FrameSlot* t = (FrameSlot*)realloc(g_frames, cap * sizeof(FrameSlot));
+    if (t) {
+      g_frames = t;
+      g_capframes = cap;
+    }
+  }
+  if (g_nframes < g_capframes) {
+    id = g_next_id++;
+    g_frames[g_nframes].id = id;
+    g_frames[g_nframes].jf = jf;
+    ++g_nframes;
+  }
+  pthread_mutex_unlock(&g_frames_mu);
+  return id;
+}
+
+/* the live frame of handle id, taken out of the table; NULL if there is none */
+static JFrame* frame_take(jlong id) {
+  JFrame* jf = NULL;
+  pthread_mutex_lock(&g_frames_mu);
+  for (size_t i = 0; i < g_nframes; ++i) {
+    if (g_frames[i].id == id) {
+      jf = g_frames[i].jf;
+      g_frames[i] = g_frames[--g_nframes];
+      break;
+    }
+  }
+  pthread_mutex_unlock(&g_frames_mu);
+  return jf;
+}
 
 /* out_rgb: a float[] (rt_render) or, u8, a byte[] (rt_render_u8); submit
  * (non-NULL): rt_render_submit_u8 into a buffer of the shim's, *submit = its
@@ -192,7 +243,8 @@ JNIEXPORT jint JNICALL Java_rtclj_Native_renderBytes(JNIEnv* env, jclass cls, jf
  * returns once the frame is on the devices (0 and a pending exception on
  * error); waitBytes blocks until it is rendered, copies its bytes into
  * outRgb (>= width x height x 3; a longer array keeps its tail) and frees
- * the handle -- every handle is waited on exactly once, from any thread. */
+ * the handle -- every handle is waited on exactly once, from any thread; a
+ * handle already waited on (or never returned) throws an argument error. */
 JNIEXPORT jlong JNICALL Java_rtclj_Native_submitBytes(JNIEnv* env, jclass cls, jfloatArray spheres, jintArray kinds,
                                                       jfloatArray mats, jfloatArray camera, jint defocus, jint width,
                                                       jint height, jint spp, jint depth, jlong seed, jint n_gpus,
@@ -201,16 +253,27 @@ JNIEXPORT jlong JNICALL Java_rtclj_Native_submitBytes(JNIEnv* env, jclass cls, j
   JFrame* jf = NULL;
   const jint rc = render_impl(env, spheres, kinds, mats, camera, defocus, width, height, spp, depth, seed, n_gpus,
                               flags, NULL, 1, &jf);
-  return rc >= 0 ? (jlong)(intptr_t)jf : 0;
+  if (rc < 0) return 0;
+  const jlong id = frame_register(jf);
+  if (!id) {   /* (no room for the handle: the frame is waited on and dropped) */
+    (void)rt_render_wait(jf->frame, NULL);
+    free(jf->buf);
+    free(jf);
+    jclass ex = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (ex) (*env)->ThrowNew(env, ex, "submitBytes: no memory for the frame's handle");
+    return 0;
+  }
+  return id;
 }
 
 JNIEXPORT jint JNICALL Java_rtclj_Native_waitBytes(JNIEnv* env, jclass cls, jlong frame, jbyteArray out_rgb) {
   (void)cls;
-  if (!frame) {
-    throw_rt(env, RT_E_ARG);
+  JFrame* jf = frame ? frame_take(frame) : NULL;
+  if (!jf) {   /* 0, a handle already waited on, or one never given out */
+    jclass ex = (*env)->FindClass(env, "java/lang/RuntimeException");
+    if (ex) (*env)->ThrowNew(env, ex, "rt error -1: waitBytes: not a frame in flight (waited on already?)");
     return RT_E_ARG;
   }
-  JFrame* jf = (JFrame*)(intptr_t)frame;
   int rc = rt_render_wait(jf->frame, NULL);   /* (the frame is consumed either way) */
   int short_out = 0;
   if (rc >= 0) {

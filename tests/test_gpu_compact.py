@@ -52,7 +52,7 @@ def cover(gpu_lib):
                                    dict(RTCLJ_COMPACT="5", RTCLJ_SPLIT="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_SPLIT="1", RTCLJ_STEAL_MIN="1", RTCLJ_SHARE_RECORDED="1"),
                                    dict(RTCLJ_COMPACT="16", RTCLJ_STEAL="0"),
-                                   dict(RTCLJ_COMPACT="0"), dict(RTCLJ_TH4="0"), dict(RTCLJ_COMPACT="1", RTCLJ_TH4="0")])
+                                   dict(RTCLJ_COMPACT="0"), dict(RTCLJ_TH4="2"), dict(RTCLJ_COMPACT="1", RTCLJ_TH4="2")])
 def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
     """Thresholds 64 (clamped: posts as full as the stack slice holds, 22 on
     this scene's tree), 16, 1 and 5; tiles kept whole and shared
@@ -60,7 +60,7 @@ def test_compaction_is_bit_exact(gpu_lib, cover, monkeypatch, knobs):
     frames of many small pools, few large ones (sample splits by default) and
     pools of 1..255 samples: each launched twice (plain order, then the
     recorded one), every frame equal to the mirror.  These small frames run
-    28 (8 x 4-pixel pools) by default; RTCLJ_TH4=0 keeps them on 22."""
+    22 by default; RTCLJ_TH4=2 moves them to 28 (8 x 4-pixel pools)."""
     from rtclj import scenes
     sc, ds = cover
     for k, v in knobs.items():

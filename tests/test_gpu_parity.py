@@ -594,13 +594,19 @@ def test_compact_variant_limits(gpu_lib):
     assert launch_variant(sc, 3840, 2160, 500) == (22, 7)   # C2 (its sums count their wraps)
     assert launch_variant(sc, 3840, 2160, 1000) == (22, 7)  # C3
     assert launch_variant(sc, 64, 36, 65536)[0] == 16       # a channel could wrap 256 times
-    # a launch of few 8 x 8 tiles (below twice the device's workgroup slots):
-    # 22's image on whole 8 x 4-pixel pools (28) instead of sample splits --
-    # C1's 8- and 4-GPU shards; a small frame too
-    assert launch_variant(sc, 1200, 84, 100) == (28, 7)
-    assert launch_variant(sc, 1200, 168, 100) == (28, 7)
-    assert launch_variant(sc, 1200, 340, 100) == (22, 7)   # (2-GPU shard: 6,375 tiles, whole 8 x 8)
-    assert launch_variant(sc, 200, 112, 100) == (28, 7)
+    # a launch of few 8 x 8 tiles stays on 22 (sample splits) by default; with
+    # RTCLJ_TH4=2 (fewer tiles than twice the device's workgroup slots) it runs
+    # 22's image on whole 8 x 4-pixel pools (28): C1's 8- and 4-GPU shards
+    assert launch_variant(sc, 1200, 84, 100) == (22, 7)
+    import os
+    os.environ["RTCLJ_TH4"] = "2"
+    try:
+        assert launch_variant(sc, 1200, 84, 100) == (28, 7)
+        assert launch_variant(sc, 1200, 168, 100) == (28, 7)
+        assert launch_variant(sc, 1200, 340, 100) == (22, 7)   # (2-GPU shard: 6,375 tiles, whole 8 x 8)
+        assert launch_variant(sc, 200, 112, 100) == (28, 7)
+    finally:
+        del os.environ["RTCLJ_TH4"]
     with variant(22):
         assert launch_variant(sc, 1200, 675, 100) == (22, 7)
         assert launch_variant(sc, 1200, 675, 255)[0] == 22
@@ -623,8 +629,8 @@ def test_compact_variant_counts_wraps(gpu_lib, scene_kind, w, h, spp):
     2^32 every ~256 bright samples and the wraps are counted per channel
     (trace_kernel.h s_carry). A sky-only frame (colour up to 1: ~4 wraps per
     channel at 1300 spp) and the cover scene at 600 spp equal the mirror bit
-    for bit, on 22 (selected) and on the default for these small frames, 28
-    (the same image on 8 x 4-pixel pools)."""
+    for bit, on 22 (the default) and on 28 (the same image on 8 x 4-pixel
+    pools)."""
     import ctypes as C
     from rtclj import raytracing as R
     from rtclj import scenes
@@ -636,7 +642,7 @@ def test_compact_variant_counts_wraps(gpu_lib, scene_kind, w, h, spp):
         sc = scenes.cover(11)
         cam = scenes.cover_camera(w, h)
     ref, segs, _ = _mirror(sc, cam, w, h, spp, 50, seed=4)
-    for vsel, want in ((0, 28), (22, 22)):
+    for vsel, want in ((0, 22), (28, 28)):
         with variant(vsel):
             ds = C.c_void_p()
             check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))

@@ -254,6 +254,13 @@ def test_submit_wait_checks_and_errors(jni):
     rc = d.Java_rtclj_Native_waitBytes(env, None, 0, barr(d, np.zeros(w * h * 3)))
     assert rc == RT_E_ARG and stats(d)["pending"]
     d.mock_clear_exception()
+    # a handle the shim never gave out (handles are ids of live frames, not
+    # pointers: ADVICE r5): an argument error, nothing dereferenced
+    for bogus in (1 << 40, -7, 0x7f00deadbeef):
+        rc = d.Java_rtclj_Native_waitBytes(env, None, bogus, barr(d, np.zeros(w * h * 3)))
+        assert rc == RT_E_ARG and stats(d)["pending"], bogus
+        assert b"not a frame in flight" in d.mock_exception_message()
+        d.mock_clear_exception()
     hd = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 4, 50, 1, 1, 0)
     st = stats(d)
     assert clean(st) and st["gets"] == 3, st
@@ -398,6 +405,10 @@ def test_shim_render_equals_rt_render(gpu_lib, jni):
         assert d.Java_rtclj_Native_waitBytes(env, None, h1, o1) == 0
         g1 = read_b(d, o1, n + 3)
         assert np.array_equal(g1[:n].reshape(h, w, 3), R.write_color(ref)) and np.all(g1[n:] == 9)
+        # waiting on a handle twice: an argument error, not a double free
+        assert not stats(d)["pending"]
+        assert d.Java_rtclj_Native_waitBytes(env, None, h1, o1) == RT_E_ARG and stats(d)["pending"]
+        d.mock_clear_exception()
         h3 = d.Java_rtclj_Native_submitBytes(env, None, sph, knd, mat, c18, cam.defocus, w, h, 8, 50, 3, 1,
                                              flags or 0)
         assert d.Java_rtclj_Native_waitBytes(env, None, h3, barr(d, np.zeros(n - 1))) == RT_E_ARG
