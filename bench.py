@@ -63,7 +63,7 @@ def metric_for(width, height, spp, depth):
     return f"Mray-samples/sec at {width}×{height}×{spp}spp depth{depth}; achieved HBM GB/s vs peak"
 
 # committed rocprofv3 PMC passes of the current build (profiles/pmc.sh), per workload
-PMC_DIRS = {"c1": ROOT / "profiles" / "r05" / "pmc_c1", "c4": ROOT / "profiles" / "r05" / "pmc_c4"}
+PMC_DIRS = {"c1": ROOT / "profiles" / "r06" / "pmc_c1", "c4": ROOT / "profiles" / "r06" / "pmc_c4"}
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector rate (packed v_pk_fma_f32)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
 FLOPS_PER_SPHERE = 17      # per-body test, a and r^2 hoisted, fma = 2
@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may run on")
     ap.add_argument("--e2e", choices=["auto", "off"], default="auto", help="time rt_render end to end on rank 0")
     ap.add_argument("--stats", choices=["auto", "off"], default="auto", help="one untimed stats-build launch")
+    ap.add_argument("--first-launch", choices=["auto", "off"], default="auto",
+                    help="time a new shape's first launch against the schedule switched off (dispatch_order); "
+                         "off for rocprof / PMC runs, whose kernel averages must be the timed frames'")
     a = ap.parse_args()
     global SAMPLER_FLAGS
     SAMPLER_FLAGS = RT_FLAG_REJECTION_SAMPLERS if a.samplers == "rejection" else 0
@@ -301,16 +304,23 @@ def _pmc_avg(pmc_dir, passes, counters):
             return None
         for r in csv.DictReader(open(f)):
             if PRODUCT_KERNEL.search(r["Kernel_Name"]) and r["Counter_Name"] in counters:
-                acc.setdefault(r["Counter_Name"], []).append((int(r.get("Dispatch_Id") or 0), float(r["Counter_Value"])))
+                acc.setdefault(r["Counter_Name"], []).append((int(r.get("Dispatch_Id") or 0),
+                                                              int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
     if any(c not in acc for c in counters):
         return None
-    # the median launch of the timed frames' recorded order: the pass's first
-    # launch runs in plain order (no tile costs yet; tile sharing adds its HBM
-    # sums, C4: 732 vs 439 MB written) and is left out when others follow
+    # the median launch of the timed frames: the pass's last launches, all of
+    # one grid (the recorded order: the units alone).  The launches before
+    # them include plain-order ones -- a new shape's, with tile sharing's
+    # helper workgroups in a larger grid and its HBM sums (C1: 20 vs 10.7 MB
+    # written; the first-launch leg's 5 pairs) -- which are left out
     out = {}
     for c, v in acc.items():
-        v = [x for _, x in sorted(v)]
-        out[c] = statistics.median(v[1:] if len(v) > 1 else v)
+        v = sorted(v)
+        grid = v[-1][1]
+        k = len(v)
+        while k > 0 and v[k - 1][1] == grid:
+            k -= 1
+        out[c] = statistics.median(x for _, _, x in v[k:])
     return out
 
 
@@ -640,11 +650,12 @@ def main():
     # order, as a process's first frame runs), timed once the GPU is warm:
     # after a launch of another shape (8 rows fewer), which makes this frame's
     # shape new again.  Alternated with the same with the schedule off
-    # (rt_set_schedule(1)), also after another shape's launch, 5 pairs; the
-    # medians are reported (single launches move by +-0.1 ms)
+    # (rt_set_schedule(1)), also after another shape's launch, 5 pairs (C1;
+    # one for the other workloads); the medians are reported (single C1
+    # launches move by +-0.1 ms)
     first_ms = plain_ms = None
     first_all, plain_all = [], []
-    if a.warmup > 0 and a.schedule == 0 and p.row_end - p.row_begin > 16:
+    if a.warmup > 0 and a.schedule == 0 and p.row_end - p.row_begin > 16 and a.first_launch == "auto":
         other = type(p).from_buffer_copy(p)
         other.row_end = p.row_end - 8
 
@@ -660,7 +671,7 @@ def main():
             return g0.elapsed_time(g1)
 
         new_shape_launch(a.schedule)   # (untimed: the first pair's launches)
-        for r in range(5):
+        for r in range(5 if a.workload == "c1" else 1):   # (one pair for the long frames)
             for sched in ((a.schedule, 1) if r % 2 == 0 else (1, a.schedule)):
                 (first_all if sched == a.schedule else plain_all).append(new_shape_launch(sched))
         first_ms = statistics.median(first_all)

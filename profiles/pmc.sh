@@ -10,7 +10,7 @@ OUT=${1:?outdir}; shift
 REPO=$PWD
 cd /tmp && export TMPDIR=/tmp && cd "$REPO" || exit 1
 mkdir -p "$OUT"
-BENCH=(python3 bench.py --cpu-baseline off --e2e off --stats off --pipelined off --sustained 0 --steps 2 --warmup 1 "$@")
+BENCH=(python3 bench.py --cpu-baseline off --e2e off --stats off --pipelined off --sustained 0 --first-launch off --steps 2 --warmup 1 "$@")
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o prof \

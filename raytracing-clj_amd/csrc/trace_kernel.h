@@ -1170,6 +1170,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
             float h, c, disc;
             body(pa + k + k, h, c, disc);
             const int sidx = *(const int __attribute__((address_space(3)))*)(uintptr_t)(pa + 64u + (k >> 1));
+            RT_MARK("exact_accept");
             consider_tie(h, disc, sidx);
           }
           RT_MARK("node");

@@ -32,8 +32,9 @@ DEFAULT_KERNEL = "_ZN5rtclj12trace_kernelILi1ELi8ELb0ELi4ELi0EEEvNS_5KArgsE"
 # loop's copy of `exact`, the tree walk's ray set-up (slab offsets, 1/u,
 # padding: read from the listing), which runs once per segment -- and goes to
 # EXCESS_TO
-PER_COPY = ("leaf", "exact")
+PER_COPY = ("leaf", "exact_tail", "exact", "exact_accept")
 EXCESS_TO = "tree_setup"
+TAIL_SPLIT = re.compile(r"v_bitop3_b32.*bitop3:0xa8")
 
 
 def blocks(isa, kernel):
@@ -58,6 +59,16 @@ def blocks(isa, kernel):
         # back to the block it branched from
         if cur == "cold" and re.match(r"\.LBB", ln):
             cur = hot   # (a PER_COPY block goes on in the same copy)
+        # the exact-test loop is rotated: its tail (root choice, acceptance,
+        # the next candidate) is laid out right after the leaf pass, whose
+        # last instruction merges the candidate mask (v_bitop3 0xa8)
+        if cur == "leaf" and TAIL_SPLIT.search(ln):
+            k0 = classify(ln)
+            if k0:
+                copies["leaf"][-1][k0] += 1
+            cur = hot = "exact_tail"
+            copies.setdefault(cur, []).append(dict(zero))
+            continue
         k = classify(ln)
         b = copies[cur][-1] if cur in PER_COPY else out.setdefault(cur, dict(zero))
         if k:
@@ -106,7 +117,8 @@ def main():
         # loop): 1 / (wave iterations per wave), from the frame's units
         per_wave = 1.0 / a.iters_per_wave
         ev = {"iteration": 1.0, "camera": pw["fresh_blocks"], "setup": 1.0, "bigleaf": 1.0, "tree_setup": 1.0,
-              "node": pw["trav_steps"], "leaf": pw["leaf_passes"], "exact": pw["exact_passes"], "hit": 1.0,
+              "node": pw["trav_steps"], "leaf": pw["leaf_passes"], "exact": pw["exact_passes"],
+              "exact_accept": pw["exact_passes"], "exact_tail": pw["exact_passes"], "hit": 1.0,
               "lambert_metal": pw["lambert_metal_blocks"], "dielectric": pw["dielectric_blocks"],
               "sums": pw.get("sums_blocks", 1.0), "refill": pw.get("refills", 1.0), "claim": pw.get("claims", 1.0),
               "drain_check": pw.get("drain_checks", 1.0),
