@@ -650,7 +650,7 @@ def main():
     # order, as a process's first frame runs), timed once the GPU is warm:
     # after a launch of another shape (8 rows fewer), which makes this frame's
     # shape new again.  Alternated with the same with the schedule off
-    # (rt_set_schedule(1)), also after another shape's launch, 5 pairs (C1;
+    # (rt_set_schedule(1)), also after another shape's launch, 9 pairs (C1;
     # one for the other workloads); the medians are reported (single C1
     # launches move by +-0.1 ms)
     first_ms = plain_ms = None
@@ -671,7 +671,7 @@ def main():
             return g0.elapsed_time(g1)
 
         new_shape_launch(a.schedule)   # (untimed: the first pair's launches)
-        for r in range(5 if a.workload == "c1" else 1):   # (one pair for the long frames)
+        for r in range(9 if a.workload == "c1" else 1):   # (one pair for the long frames)
             for sched in ((a.schedule, 1) if r % 2 == 0 else (1, a.schedule)):
                 (first_all if sched == a.schedule else plain_all).append(new_shape_launch(sched))
         first_ms = statistics.median(first_all)
@@ -830,7 +830,7 @@ def main():
                                "note": "the first launch of a new shape (no tile costs yet: tiles in plain dispatch "
                                        "order, as a process's first frame runs), timed after the GPU is warm, right "
                                        "after a launch of another shape; plain_schedule_off_ms: the same frame with "
-                                       "the schedule off (rt_set_schedule(1)), also a new shape; medians of 5 "
+                                       "the schedule off (rt_set_schedule(1)), also a new shape; medians of 9 "
                                        "alternated pairs (events around the whole rt_launch: its fills and kernels); "
                                        "the timed steps dispatch longest first by the previous launches' per-tile "
                                        "durations (each added to half the record before it)"},
