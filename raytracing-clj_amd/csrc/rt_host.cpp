@@ -22,6 +22,7 @@
 #include <deque>
 #include <functional>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -449,6 +450,38 @@ int get_scene(int device, const rt_scene* s, std::shared_ptr<rt_dscene>* out, bo
   return RT_OK;
 }
 
+// A render context's stream: non-blocking, at the device's highest priority.
+// The HIP runtime maps a process's streams onto a few hardware queues per
+// priority level (GPU_MAX_HW_QUEUES, 4) and, once a level's queues exist,
+// adds a new stream to one already in use.  A process that has run work on
+// other streams (an application's own, bench.py's pipelined leg) then puts two
+// frames in flight on one queue, where frame k's D2H, enqueued at
+// rt_render_wait, waits behind frame k+1's kernel and the frame loop loses its
+// overlap: C1 in flight 4.97 ms per frame at normal priority after bench.py's
+// pipelined leg, 4.73-4.74 at high priority (or with a full CU mask, a queue
+// of its own but a blocking stream), 4.69-4.72 in a fresh process either way
+// (profiles/r06/inflight/).  RTCLJ_CTX_STREAM (A/B): 0 = normal priority,
+// 1 = full CU mask.
+hipError_t make_stream(int device, hipStream_t* s) {
+  const char* v = std::getenv("RTCLJ_CTX_STREAM");
+  const int kind = v ? std::atoi(v) : 2;
+  if (kind == 1) {
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+    for (int k = 0; k < prop.multiProcessorCount; ++k) mask[k / 32] |= 1u << (k % 32);
+    return hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data());
+  }
+  if (kind == 2) {
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e != hipSuccess) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 std::unique_ptr<Ctx> take_ctx(int device) {
   DeviceCache& dc = (*g_cache)[device];
   {
@@ -467,7 +500,7 @@ std::unique_ptr<Ctx> take_ctx(int device) {
       std::unique_ptr<Ctx> c = std::move(dc.primary);
       lk.unlock();
       hipStream_t s = nullptr;
-      if (hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+      if (hipSetDevice(device) == hipSuccess && make_stream(device, &s) == hipSuccess) {
         rebind_stream_schedules(nullptr, s, c->scenes.data(), static_cast<int>(c->scenes.size()));
         c->stream = s;
         c->null_stream = false;
@@ -580,7 +613,7 @@ void start_shard(const rt_scene* s, const rt_camera* c, Shard* sh, void* out_rgb
   Ctx* cx = sh->cx.get();
   const size_t nfl = static_cast<size_t>(sh->rows) * sh->p.width * 3;
   hipError_t e = hipSetDevice(sh->device);
-  if (e == hipSuccess && !cx->stream && !cx->null_stream) e = hipStreamCreateWithFlags(&cx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess && !cx->stream && !cx->null_stream) e = make_stream(sh->device, &cx->stream);
   if (e == hipSuccess && !cx->e0) e = hipEventCreate(&cx->e0);
   if (e == hipSuccess && !cx->e1) e = hipEventCreate(&cx->e1);
   if (e == hipSuccess && !cx->eg) e = hipEventCreate(&cx->eg);

@@ -663,6 +663,34 @@ static int launch_slots(int device, const void* fn, size_t lds, int threads = 25
   return cus * per;
 }
 
+// the most splits of one tile (rt_launch's sample split, below)
+constexpr int kSplitMax = 64;
+
+// The pending sort of a stream's tile-cost record (Schedule::sort_pending):
+// order_kernel, and plan_kernel for a planned split; the order is ready for
+// the next launch of the shape.  Returns the launches' hipError_t.
+static int sort_record(Schedule* sch, int n_tiles, int spp, hipStream_t stream) {
+  unsigned* cost = sch->cost;
+  int* order = sch->order;
+  int n = n_tiles;
+  void* sargs[] = {&cost, &order, &n};
+  hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream);
+  if (e != hipSuccess) return e;
+  sch->ready = true;
+  sch->sort_pending = false;
+  sch->plan_units = -1;
+  if (sch->sort_plan > 0 && sch->units_cap >= sch->sort_plan) {
+    // the next split launch's cost-balanced units, from this record
+    int2* units = sch->units;
+    int Uk = sch->sort_plan, smax = std::min(spp, kSplitMax);
+    void* pargs[] = {&cost, &order, &n, &Uk, &smax, &units};
+    e = hipLaunchKernel(reinterpret_cast<const void*>(&plan_kernel), dim3(1), dim3(1024), pargs, 0, stream);
+    if (e != hipSuccess) return e;
+    sch->plan_units = sch->sort_plan;
+  }
+  return hipSuccess;
+}
+
 // the variants of the compact image (u8 node-index stack, u32 sums)
 static bool compact_variant(int v) { return v == 22 || v == 24 || v == 26 || v == 28; }
 
@@ -814,7 +842,7 @@ static uint64_t magic64(int d) { return d <= 1 ? 0 : ~0ull / static_cast<uint64_
 // (at most kSplitMax).  tools/shard_time.py on C1's 1/2/4/8-GPU shards
 // (profiles/r02/shard_split_rounds.txt): 3-4 rounds best (8 GPUs: 5.88x at 3,
 // 5.72x at 4, 5.30x at 6, 3.96x at 16; unsplit 2.57x)
-constexpr int kSplitMax = 64;
+// (kSplitMax, the most splits of a tile: defined above sort_record)
 
 namespace rtclj {
 int fill_async(void* p, int byte_value, size_t bytes, void* stream) {
@@ -1052,24 +1080,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       HIP_TRY(hipMalloc(&sch->order, n_tiles * sizeof(int)));
       sch->cap = n_tiles;
     }
-    if (sch->sort_pending) {   // the previous launch's record, sorted now (stream-ordered after it)
-      unsigned* cost = sch->cost;
-      int* order = sch->order;
-      int n = n_tiles;
-      void* sargs[] = {&cost, &order, &n};
-      HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&order_kernel), dim3(1), dim3(1024), sargs, 0, stream));
-      sch->ready = true;
-      sch->sort_pending = false;
-      sch->plan_units = -1;
-      if (sch->sort_plan > 0 && sch->units_cap >= sch->sort_plan) {
-        // the next split launch's cost-balanced units, from this record
-        int2* units = sch->units;
-        int Uk = sch->sort_plan, smax = std::min(p->spp, kSplitMax);
-        void* pargs[] = {&cost, &order, &n, &Uk, &smax, &units};
-        HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&plan_kernel), dim3(1), dim3(1024), pargs, 0, stream));
-        sch->plan_units = sch->sort_plan;
-      }
-    }
+    // the previous launch's record, sorted now (stream-ordered after it)
+    if (sch->sort_pending) HIP_TRY(static_cast<hipError_t>(sort_record(sch, n_tiles, p->spp, stream)));
     if (sch->ready) a.tile_order = sch->order;
     a.tile_cost = sch->cost;
     // a split launch in the recorded order: with RTCLJ_SPLIT_PLAN=1, the
@@ -1201,6 +1213,8 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   if (a.tile_cost) {
     // this record's sort, at the next launch of the shape on the stream
+    // (RTCLJ_SORT_EAGER=1, A/B: right behind this launch, as before round 6;
+    // within noise on every bench.py leg, profiles/r06/sort_ab/)
     sch->sort_pending = true;
     sch->ready = false;
     sch->sort_plan = -1;
@@ -1216,6 +1230,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
       }
       sch->sort_plan = U;
     }
+    if (env_int("RTCLJ_SORT_EAGER", 0, 0) != 0) HIP_TRY(static_cast<hipError_t>(sort_record(sch, n_tiles, p->spp, stream)));
   }
   HIP_TRY(hipGetLastError());
   return RT_OK;
