@@ -386,6 +386,13 @@ int rt_debug_waves(int device, uint64_t* out, size_t n_waves);
  * counts.  Timing only: the bits never depend on it. */
 int rt_steal_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2);
 
+/* Path export of rt_launch's split launches (diagnostic; RTCLJ_EXPORT=1):
+ * out2[0] = the launches on (ds, hip_stream) since the last call that wrote
+ * their waves' last paths out for a sweep launch, out2[1] =
+ * the records the latest of them wrote.  Waits for the stream.  Timing
+ * only: the bits never depend on it. */
+int rt_export_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2);
+
 /* A device's one-time start-up, done ahead of the first render so that a
  * one-frame process (-main, raytracing.clj:95-177) can overlap it with its
  * own work (rt_main starts it on a thread at process start): the device

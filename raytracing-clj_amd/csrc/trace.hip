@@ -242,7 +242,8 @@ static const Variant& variant_table(int v) {
   static const Variant v16{RT_K(SRC_LDS, SCAN_BVHQ, false), true, false, SCAN_BVHQ};
   // (8-wave workgroups: one tree image for twice the waves)
   static const Variant v18{RT_KW(SRC_LDS, SCAN_BVHO, false, 8), true, false, SCAN_BVHO, 512};
-  static const Variant v22{RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7};
+  static const Variant v22{RT_K(SRC_LDS, SCAN_BVHQ7, false), true, false, SCAN_BVHQ7, 256, 0,
+                           RT_KSW(SRC_LDS, SCAN_BVHQ7, 4, 0)};
   // (22's image in 8-wave workgroups: one tree image per 8 waves, for trees
   // too big for 22's 4-wave workgroups)
   static const Variant v24{RT_KW(SRC_LDS, SCAN_BVHQ7, false, 8), true, false, SCAN_BVHQ7, 512};
@@ -350,6 +351,12 @@ struct Schedule {
   int2* units = nullptr;                // cost-balanced split plan (plan_kernel) of the next split launch
   int units_cap = 0;
   int plan_units = -1;                  // the plan's unit count (-1: none)
+  // path export (KArgs xq, xq_n): the records of a split launch's exported
+  // paths, and [written, the sweep's claims] (zeroed before each launch)
+  uint4* xq = nullptr;
+  size_t xq_cap = 0;                    // records
+  unsigned* xq_n = nullptr;
+  unsigned long long xq_launches = 0;   // export launches since rt_export_stats
 };
 constexpr int kSchedStreams = 16;
 struct ScheduleSet {
@@ -366,6 +373,8 @@ struct ScheduleSet {
     if (e.owner) (void)hipFree(e.owner);
     if (e.stealc) (void)hipFree(e.stealc);
     if (e.units) (void)hipFree(e.units);
+    if (e.xq) (void)hipFree(e.xq);
+    if (e.xq_n) (void)hipFree(e.xq_n);
     e = Schedule{};
   }
   void release() {
@@ -963,8 +972,10 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
 #else
   const size_t lds = launch_lds(*ds, vsel);
 #endif
-  if (lds > 64 * 1024)
+  if (lds > 64 * 1024) {
     HIP_TRY(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+    if (v.sweep) HIP_TRY(hipFuncSetAttribute(v.sweep, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  }
   // the stream's entry: adaptive schedule and split partial sums
   Schedule* sch = nullptr;
   std::unique_lock<std::mutex> sched_lock;
@@ -1190,6 +1201,29 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // batches were round 3's: C1 5.960 -> 5.916 ms, C2 287.9 -> 286.1 ms,
   // profiles/r04/lds_batch/)
   a.lds_batch_max = std::max(64, env_int("RTCLJ_LDS_BATCH", 256, 64));
+  // Path export for split launches (KArgs xq; RTCLJ_EXPORT=1, A/B): a wave
+  // whose batches are spent and which holds at most RTCLJ_EXPORT_LIM paths
+  // (default 64: as soon as its batches are spent) writes them out and
+  // leaves, so a unit's workgroup frees its slot without draining; the sweep
+  // launch runs the records.  At most one record per thread of a unit.
+  const bool xport = split > 1 && v.sweep && env_int("RTCLJ_EXPORT", 0, 0) != 0;
+  if (xport) {
+    const size_t need = static_cast<size_t>(n_units) * v.threads;
+    if (sch->xq_cap < need) {   // grow: this stream's kernels may still read the old records
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (sch->xq) (void)hipFree(sch->xq);
+      sch->xq = nullptr;
+      sch->xq_cap = 0;
+      HIP_TRY(hipMalloc(&sch->xq, need * 4 * sizeof(uint4)));
+      sch->xq_cap = need;
+    }
+    if (!sch->xq_n) HIP_TRY(hipMalloc(&sch->xq_n, 2 * sizeof(unsigned)));
+    fills.add(sch->xq_n, 0, 2 * sizeof(unsigned));
+    a.xq = sch->xq;
+    a.xq_n = sch->xq_n;
+    a.compact = std::min(64, env_int("RTCLJ_EXPORT_LIM", 64, 1));
+    ++sch->xq_launches;
+  }
   if (fills.count) {
     size_t most = 0;
     for (int k = 0; k < fills.count; ++k) most = std::max(most, fills.n[k]);
@@ -1201,6 +1235,20 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   void* args[] = {&a};
   if (split > 1) sch->part_dirty = true;   // (cleared once finalize_kernel is enqueued)
   HIP_TRY(hipLaunchKernel(v.fn, dim3(static_cast<unsigned>(grid)), block, args, lds, stream));
+  if (xport) {
+    // the sweep: one workgroup per slot the device holds, each starting on
+    // its own 256 records and claiming more; a workgroup past the records
+    // leaves at once.  It adds into part[], so it runs before finalize_kernel.
+    KArgs b = a;
+    b.word = nullptr;
+    b.tile_cost = nullptr;
+    b.tile_order = nullptr;
+    b.unit_tab = nullptr;
+    b.compact = is_bvh_scan(v.scan) ? std::min(b.mb_paths, env_int("RTCLJ_COMPACT", b.mb_paths, 0)) : 0;
+    const int sw = std::max(1, launch_slots(ds->device, v.sweep, lds, v.threads));
+    void* bargs[] = {&b};
+    HIP_TRY(hipLaunchKernel(v.sweep, dim3(static_cast<unsigned>(sw)), block, bargs, lds, stream));
+  }
   if (split > 1) {
     unsigned long long* part = a.part;
     const int* order = a.tile_order;
@@ -1310,6 +1358,29 @@ extern "C" int rt_steal_stats(const rt_dscene* ds, void* hip_stream, uint64_t* o
     HIP_TRY(hipStreamSynchronize(stream));
     HIP_TRY(hipMemcpy(out2, e.stealc, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(e.stealc, 0, 2 * sizeof(uint64_t)));
+  }
+  return RT_OK;
+}
+
+// Path export of the split launches on (ds, stream) (diagnostic): out2 =
+// {export launches since the last call, records the latest one wrote}; waits
+// for the stream.
+extern "C" int rt_export_stats(const rt_dscene* ds, void* hip_stream, uint64_t* out2) {
+  clear_error();
+  if (!ds || !out2) return set_error(RT_E_ARG, "rt_export_stats: NULL argument");
+  out2[0] = out2[1] = 0;
+  const hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+  std::lock_guard<std::mutex> lk(ds->sched.mu);
+  for (int k = 0; k < ds->sched.used; ++k) {
+    Schedule& e = ds->sched.s[k];
+    if (e.stream != stream || !e.xq_n) continue;
+    HIP_TRY(hipSetDevice(ds->device));
+    HIP_TRY(hipStreamSynchronize(stream));
+    unsigned n[2] = {0, 0};
+    HIP_TRY(hipMemcpy(n, e.xq_n, sizeof n, hipMemcpyDeviceToHost));
+    out2[0] = e.xq_launches;
+    out2[1] = n[0];
+    e.xq_launches = 0;
   }
   return RT_OK;
 }

@@ -141,6 +141,16 @@ struct alignas(16) KArgs {
   // its traversal stack's LDS and leaves (0: off; <= mb_paths)
   int compact;
   int mb_paths;   // paths a post holds: as many as the wave's stack slice has room for (<= 32)
+  // Path export (split launches).  xq non-NULL: a wave whose
+  // batches are spent and which holds at most `compact` paths writes them to
+  // xq as 64-byte records (xq_n[0] counts them) and leaves, so that its
+  // workgroup's slot is free as soon as its pool is spent; the sweep launch
+  // that follows (trace_kernel<..., SWEEP>) runs the records to their ends,
+  // its waves claiming 64 at a time from xq_n[1], and adds their colours to
+  // part[].  A record: origin, direction, throughput, RNG state, the pixel
+  // (compacted row x width + column), depth left, the body it leaves.
+  uint4* xq;
+  unsigned* xq_n;
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -457,7 +467,7 @@ __device__ void diag_scan(const struct KArgs& a, const float4* s_geo, float ox, 
 // workgroups = 8 waves per SIMD, where 4-wave workgroups fit 3 per CU)
 // THT: the pool's tile rows (0: tile_rows(SCAN); variant 28 runs 22's
 // compact image on 8 x 4-pixel pools, for launches of few 8 x 8 tiles)
-template <int SRC, int SCAN, bool STATS = false, int NW = 4, int THT = 0>
+template <int SRC, int SCAN, bool STATS = false, int NW = 4, int THT = 0, bool SWEEP = false>
 __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_kernel(const KArgs a) {
   constexpr int NT = 64 * NW;   // threads
   // The sample pool: the workgroup's 8 x 8 pixels x spp samples are the
@@ -515,7 +525,14 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // (set-up and epilogue arguments through an opaque pointer: re-loaded
   // where used, not kept in SGPRs across the hot loop)
   const KArgsP ka = kargs_opaque();
-  const bool own = unit < ka->n_units;
+  const bool own = SWEEP || unit < ka->n_units;
+  // the sweep: the records the launch before wrote; workgroup u starts on
+  // records [u * NT, (u + 1) * NT)
+  int xpool = 0;
+  if constexpr (SWEEP) {
+    xpool = static_cast<int>(__hip_atomic_load(&ka->xq_n[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (unit * NT >= xpool) return;
+  }
   // samples of whole tile t (its in-image pixels x spp)
   auto tile_pool = [&](KArgsP kp, int t) {
     const int ty = t / kp->tiles_x, tx = t - ty * kp->tiles_x;
@@ -633,9 +650,11 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
 
   // the unit: a whole tile or one sample split of a tile at the order's end
   // (own), or a stolen sample range [first, s_lim) of a whole tile
-  int tile, split_ix = 0, first = 0, nsplit = 1;
+  int tile = 0, split_ix = 0, first = 0, nsplit = 1;
   bool split = false;
-  if (own) {
+  if constexpr (SWEEP) {
+    first = unit * NT;
+  } else if (own) {
     int pos = unit;
     split = unit >= ka->n_whole;
     if (split && ka->unit_tab) {   // a cost-balanced split
@@ -684,7 +703,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // pool index j -> (pixel q = j % npx, sample k0 + j / npx); the next free
   // index is `base`.  j / npx by a 64-bit magic (exact for every 32-bit j);
   // q / vw by multiply-high (exact: q < 64, vw <= 8)
-  const int pool = (cnt > 0 && ka->max_depth > 0) ? npx * cnt : 0;
+  const int pool = SWEEP ? xpool : (cnt > 0 && ka->max_depth > 0) ? npx * cnt : 0;
   const uint32_t mag_vw = vw > 0 ? 0xffffffffu / static_cast<uint32_t>(vw) + 1u : 0u;
   const uint32_t mag16_vw = vw > 0 ? (65536u + static_cast<uint32_t>(vw) - 1u) / static_cast<uint32_t>(vw) : 0u;
   const uint64_t npx_magic = npx > 1 ? ~0ull / static_cast<uint64_t>(npx) + 1ull : 0ull;
@@ -698,7 +717,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // publish: an earlier unit ends while later ones still start, so no helper
   // would ever join it, and its claims would all be HBM atomics (C4: ~60 per
   // tile, 3 GB of WRITE_SIZE per launch when every unit published).
-  const bool shared_tile = ka->word && !split && (!own || (pool > 512 && unit >= ka->share_from));
+  const bool shared_tile = !SWEEP && ka->word && !split && (!own || (pool > 512 && unit >= ka->share_from));
   // where the waves claim their batches: the shared tile's word, else (NULL)
   // the workgroup's s_pool_next
   unsigned long long* const src = shared_tile ? ka->word + tile : nullptr;
@@ -727,7 +746,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // key and coordinates, so a camera sample costs one LDS read instead of
   // the index arithmetic and two hashes (the 8-body-leaf traversal, whose
   // workgroups are register-bound, computes them instead)
-  constexpr bool kPixelTable = is_q(SCAN);
+  constexpr bool kPixelTable = is_q(SCAN) && !SWEEP;
   // (the compact variant: the keys alone, 4 bytes a pixel, and the image row
   // of each of the tile's rows as a float; a pixel's column is q mod vw)
   constexpr bool kCompactPx = SCAN == SCAN_BVHQ7;
@@ -810,6 +829,34 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
     const int left = static_cast<int>(__popcll(live));
     bool out = false;   // counted out, and the last wave to do so
     bool post = false;
+    if constexpr (!SWEEP) {
+      // path export (KArgs::xq): the wave's paths out to HBM records, for
+      // the sweep launch; the wave leaves
+      uint4* const xq = kargs_opaque()->xq;
+      if (xq) {
+        if (left > 0) {
+          int base = 0;
+          if (lane == leader) base = static_cast<int>(atomicAdd(&kargs_opaque()->xq_n[0], static_cast<unsigned>(left)));
+          base = __builtin_amdgcn_readlane(base, leader);
+          const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(live >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(live), 0u)));
+          if (active) {
+            // the pixel: compacted row x width + column (q / vw as the camera sample's multiply-high)
+            const int qy = static_cast<int>(__umul24(static_cast<uint32_t>(q), mag16_vw) >> 16);
+            const int pix = (qy0 + qy) * kargs_opaque()->width + qx0 + (q - qy * vw);
+            uint4* r = xq + 4 * static_cast<size_t>(base + rank);
+            r[0] = make_uint4(__float_as_uint(ox), __float_as_uint(oy), __float_as_uint(oz), __float_as_uint(dx));
+            r[1] = make_uint4(__float_as_uint(dy), __float_as_uint(dz), __float_as_uint(tr), __float_as_uint(tg));
+            r[2] = make_uint4(__float_as_uint(tb), st, static_cast<uint32_t>(pix), static_cast<uint32_t>(rem));
+            reinterpret_cast<uint32_t*>(r + 3)[0] = static_cast<uint32_t>(last);
+          }
+        }
+        if (lane == leader) atomicAdd(&s_alive, -1);
+        active = false;
+        j = -2;
+        return;
+      }
+    }
     if (left > 0 && left <= sgpr(lds_load(&s_mb_lim[wu]))) {
       post = sgpr(lds_load(&s_alive)) > 1;
       // posting now; or alone (no sibling will ever take them): not again
@@ -915,6 +962,26 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
     RT_MARK("iteration");
     if (kCompact ? j >= 0 : fresh) {
       RT_MARK("camera");
+      if constexpr (SWEEP) {   // a record of the launch before: the path as it left its wave
+        const uint4* r = kargs_opaque()->xq + 4 * static_cast<size_t>(j);
+        const uint4 r0 = r[0], r1 = r[1], r2 = r[2];
+        const uint32_t r3 = reinterpret_cast<const uint32_t*>(r + 3)[0];
+        ox = __uint_as_float(r0.x);
+        oy = __uint_as_float(r0.y);
+        oz = __uint_as_float(r0.z);
+        dx = __uint_as_float(r0.w);
+        dy = __uint_as_float(r1.x);
+        dz = __uint_as_float(r1.y);
+        tr = __uint_as_float(r1.z);
+        tg = __uint_as_float(r1.w);
+        tb = __uint_as_float(r2.x);
+        st = r2.y;
+        q = static_cast<int>(r2.z);
+        rem = static_cast<int>(r2.w);
+        last = static_cast<int>(r3);
+        fresh = false;
+        j = -1;
+      } else {
       if constexpr (STATS) {
         const uint64_t ex = __builtin_amdgcn_read_exec();
         if (lane == __ffsll(static_cast<long long>(ex)) - 1) {
@@ -991,6 +1058,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       last = -1;
       fresh = false;
       if constexpr (kCompact) j = -1;
+      }
     }
 
 
@@ -1579,7 +1647,13 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
       if constexpr (STATS) st_fl += 3;
       if constexpr (STATS) wave_event(st_sums);
       AccT* acc = &s_acc[q * 3];
-      if (kCompactPx && sgpr(kargs_opaque()->spp) > 255) {
+      if constexpr (SWEEP) {   // a record's path: into its pixel's split sums in HBM
+        unsigned long long* pp = kargs_opaque()->part + static_cast<size_t>(q) * 3;
+        const uint32_t f0 = fix24(cr), f1 = fix24(cg), f2 = fix24(cb);
+        if (f0) __hip_atomic_fetch_add(pp + 0, static_cast<unsigned long long>(f0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f1) __hip_atomic_fetch_add(pp + 1, static_cast<unsigned long long>(f1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f2) __hip_atomic_fetch_add(pp + 2, static_cast<unsigned long long>(f2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (kCompactPx && sgpr(kargs_opaque()->spp) > 255) {
         // the u32 sums with their wraps counted (s_carry above)
         const uint32_t f0 = fix24(cr), f1 = fix24(cg), f2 = fix24(cb);
         const uint32_t o0 = __hip_atomic_fetch_add(acc + 0, f0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1638,13 +1712,15 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
             g = static_cast<int>(static_cast<unsigned>(wd));
             if (g < pool) atomicAdd(&s_cnt, min(pool - g, want));
             atomicMax(&s_join, word_helpers(wd));
+          } else if constexpr (SWEEP) {   // records past the grid's first ones, 64 at a time
+            g = static_cast<int>(atomicAdd(&kargs_opaque()->xq_n[1], 64u)) + static_cast<int>(gridDim.x) * NT;
           } else {
             g = atomicAdd(&s_pool_next, want);
           }
         }
         g = __builtin_amdgcn_readlane(g, leader);
         wb = min(g, pool);
-        we = min(g + want, pool);
+        we = min(g + (SWEEP ? 64 : want), pool);
         if (wb >= pool) we = pool;   // spent: the lanes left over retire
       }
       RT_MARK("refill");
@@ -1701,6 +1777,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   // 8 pixels are 24 consecutive floats
   __syncthreads();
   const KArgsP ke = kargs_opaque();
+  if constexpr (!SWEEP) {
   const int t = static_cast<int>(threadIdx.x);
   // (owner of an unshared tile: no helper joined before its pool was spent)
   const bool alone = !shared_tile || sgpr(s_join) == 0;
@@ -1764,6 +1841,7 @@ __global__ __launch_bounds__(64 * NW, min_waves(SCAN, STATS, NW)) void trace_ker
   }
   if (ke->counters && own && threadIdx.x == 0 && pool)
     atomicAdd(&ke->counters[1], static_cast<unsigned long long>(pool));
+  }   // (!SWEEP: a sweep's colours went to part[] as its paths ended)
 
   if constexpr (STATS) {
     if (a.dbg && st_iter) {
@@ -1869,11 +1947,13 @@ struct Variant {
   int scan;   // SCAN_* (the tile shape: tile_rows, unless th)
   int threads = 256;   // workgroup size
   int th = 0;          // the pool's tile rows (0: tile_rows(scan))
+  const void* sweep = nullptr;   // the variant's sweep kernel (path export, KArgs::xq), or NULL
 };
 inline int variant_rows(const Variant& v) { return v.th ? v.th : tile_rows(v.scan); }
 #define RT_K(SRC, SCAN, ST) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST>)
 #define RT_KW(SRC, SCAN, ST, NW) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST, NW>)
 #define RT_KWT(SRC, SCAN, ST, NW, TH) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, ST, NW, TH>)
+#define RT_KSW(SRC, SCAN, NW, TH) reinterpret_cast<const void*>(&trace_kernel<SRC, SCAN, false, NW, TH, true>)
 // The diagnostic library's variants (trace_diag.hip): v's entry, or NULL.
 const Variant* diag_variant(int v);
 

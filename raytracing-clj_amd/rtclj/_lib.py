@@ -105,6 +105,7 @@ SIGNATURES = {
     "rt_debug_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
     "rt_debug_waves": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.c_size_t]),
     "rt_steal_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]),
+    "rt_export_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]),
     "rt_device_count": (C.c_int, []),
     "rt_last_error": (C.c_char_p, []),
     "rt_version": (C.c_char_p, []),

@@ -38,10 +38,14 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None, help="override the workload's max depth (not a bench line)")
     ap.add_argument("--row-tile", type=int, default=8, help="rows per interleaved shard tile")
     ap.add_argument("--inflight", type=int, nargs="+", default=[0],
                     help="stream counts for the pipelined measurement (0: off)")
     ap.add_argument("--frames", type=int, default=40)
+    ap.add_argument("--b2b", type=int, default=0,
+                    help="also time this many launches back to back on the one stream (bench.py's timed steps: "
+                         "the host's enqueue overlaps the device), per frame")
     ap.add_argument("--no-streamed-flag", action="store_true",
                     help="pipelined launches without RT_FLAG_STREAMED (the single-frame split policy)")
     ap.add_argument("--configs", nargs="*", default=[""],
@@ -51,15 +55,19 @@ def main():
     W = wl["width"]
     H = R.image_height(W)
     spp = a.spp or wl["spp"]
+    if a.depth:
+        wl = dict(wl, depth=a.depth)
     sc = scenes.cover_c4() if wl["scene"] == "c4" else scenes.cover(11, 42)
     cam = scenes.cover_camera(W, H)
     stream = torch.cuda.current_stream()
     sh = C.c_void_p(stream.cuda_stream)
     import os
     allres = []
+    base = {k: v for k, v in os.environ.items() if k.startswith("RTCLJ_")}   # the caller's settings
     for cfg in a.configs:
-        for k in [k for k in os.environ if k.startswith("RTCLJ_") and k != "RTCLJ_SPLIT_ROUNDS"]:
+        for k in [k for k in os.environ if k.startswith("RTCLJ_")]:
             del os.environ[k]
+        os.environ.update(base)
         for kv in filter(None, cfg.split(",")):
             k, v = kv.split("=")
             os.environ[k] = v
@@ -71,11 +79,11 @@ def main():
 
 
 def run(a, wl, W, H, spp, sc, cam, sh, stream):
-    res = {"workload": a.workload, "spp": spp, "worlds": {}}
+    res = {"workload": a.workload, "spp": spp, "depth": wl["depth"], "worlds": {}}
     t1 = None
     t1p = {}
     for n in a.worlds:
-        per, per_pipe = [], {}
+        per, per_pipe, per_b2b = [], {}, []
         for r in range(n):
             ds = C.c_void_p()
             check(lib.rt_scene_upload(0, C.byref(sc.c), C.byref(ds)))
@@ -98,6 +106,14 @@ def run(a, wl, W, H, spp, sc, cam, sh, stream):
                 torch.cuda.synchronize()
                 ts.append(s.elapsed_time(e))
             per.append(statistics.median(ts))
+            if a.b2b > 0:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record(stream)
+                for _ in range(a.b2b):
+                    launch()
+                e.record(stream)
+                torch.cuda.synchronize()
+                per_b2b.append(s.elapsed_time(e) / a.b2b)
             for nin in a.inflight:
                 if nin <= 0:
                     continue
@@ -128,6 +144,14 @@ def run(a, wl, W, H, spp, sc, cam, sh, stream):
         res["worlds"][n] = {"max_ms": mx, "mean_ms": sum(per) / n, "per_rank_ms": per,
                             "speedup": (t1 / mx) if t1 else None}
         msg = f"N={n}: max {mx:.3f} ms mean {sum(per) / n:.3f} ms speedup {t1 / mx if t1 else 0:.2f}"
+        if per_b2b:
+            mb = max(per_b2b)
+            if n == 1:
+                t1b = mb
+                res["t1_b2b"] = mb
+            t1b = res["t1_b2b"]
+            res["worlds"][n]["b2b"] = {"max_ms": mb, "per_rank_ms": per_b2b, "speedup": t1b / mb}
+            msg += f" | back to back: {mb:.3f} ms/frame x{t1b / mb:.2f}"
         for nin, pp in per_pipe.items():
             pm = max(pp)
             if n == 1:
