@@ -115,7 +115,7 @@ SIGNATURES = {
 RT_ABI_VERSION = 3   # include/rt.h; the structures above are this revision's
 # functions added within the revision (a build from before them still loads)
 ADDITIVE = {"rt_prepare", "rt_render_u8", "rt_quantize_device", "rt_render_submit", "rt_render_submit_u8",
-            "rt_render_wait"}
+            "rt_render_wait", "rt_export_stats"}
 
 
 def load(path: Path) -> C.CDLL:
