@@ -106,6 +106,13 @@ struct FillSet {
     ++count;
   }
 };
+// A shape's first order, before any record: the tiles bottom-up
+// (order[i] = n - 1 - i)
+__global__ __launch_bounds__(256) void iota_rev_kernel(int* __restrict__ order, int n) {
+  const int i = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  if (i < n) order[i] = n - 1 - i;
+}
+
 __global__ __launch_bounds__(256) void fill_set_kernel(const FillSet f) {
   const size_t stride = static_cast<size_t>(gridDim.x) * 256;
   for (int k = 0; k < f.count; ++k)
@@ -1077,6 +1084,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   }
   // the fills this launch needs before its trace kernel, as one launch
   FillSet fills;
+  bool first_order = false;   // a shape's first launch in a heuristic order
   if (sch && g_schedule.load() == 0) {
     if (sch->cap < n_tiles) {   // grow: this stream's kernels may still read the old buffers
       HIP_TRY(hipStreamSynchronize(stream));
@@ -1093,7 +1101,24 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     }
     // the previous launch's record, sorted now (stream-ordered after it)
     if (sch->sort_pending) HIP_TRY(static_cast<hipError_t>(sort_record(sch, n_tiles, p->spp, stream)));
-    if (sch->ready) a.tile_order = sch->order;
+    if (sch->ready) {
+      a.tile_order = sch->order;
+    } else if (env_int("RTCLJ_FIRST_ORDER", 1, 0) == 1) {
+      // No record yet: the tiles bottom-up.  The reference's scenes (and
+      // C1-C4) put the ground and its bodies below the sky: the expensive
+      // tiles start first and the launch ends on sky tiles, where row-major
+      // order ended on the ground's.  C1's first frame of a shape 5.13-5.19
+      // ms against 5.25 row-major (tools/first_frame.py, 9 pairs, two
+      // rounds; profiles/r06/first_order/); RTCLJ_FIRST_ORDER=0: row-major.
+      // Tile sharing still balances the tail, as in plain order.
+      int* order = sch->order;
+      int n = n_tiles;
+      void* oargs[] = {&order, &n};
+      HIP_TRY(hipLaunchKernel(reinterpret_cast<const void*>(&iota_rev_kernel), dim3(static_cast<unsigned>((n + 255) / 256)),
+                              dim3(256), oargs, 0, stream));
+      a.tile_order = sch->order;
+      first_order = true;
+    }
     a.tile_cost = sch->cost;
     // a split launch in the recorded order: with RTCLJ_SPLIT_PLAN=1, the
     // cost-balanced units the previous launch of the shape planned (when it
@@ -1116,7 +1141,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
   // 5.94 ms either way), while its claims and helpers' scans are HBM atomics
   // (C1: 31 vs 11 MB per launch; profiles/r04/share_rounds/): off there
   // unless RTCLJ_SHARE_RECORDED=1.
-  if (steal && split == 1 && (!a.tile_order || env_int("RTCLJ_SHARE_RECORDED", 0, 0) != 0)) {
+  if (steal && split == 1 && (!a.tile_order || first_order || env_int("RTCLJ_SHARE_RECORDED", 0, 0) != 0)) {
     const int slots = std::max(1, launch_slots(ds->device, v.fn, lds, v.threads));
     const int n_owner = 2 * slots;   // owner entries: twice the resident workgroups
     // (at most 32 per slot: a tile's helper count stays below 2^16)
@@ -1193,7 +1218,7 @@ extern "C" int rt_launch(const rt_dscene* ds, const rt_camera* c, const rt_param
     // order up to 1/48 of the tile's pool (0: the kernel's per-pool rule; C1's
     // 6,400: 128 -- helpers then need small claims to balance the tail;
     // C4's 64,000: 1024)
-    a.batch_max = env_int("RTCLJ_BATCH_MAX", a.tile_order ? 1024 : 0, 0);
+    a.batch_max = env_int("RTCLJ_BATCH_MAX", (a.tile_order && !first_order) ? 1024 : 0, 0);
   }
   a.n_units = n_units;
   // a wave's claims on an unshared pool: guided (an eighth of what is left
