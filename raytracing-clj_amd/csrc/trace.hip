@@ -38,17 +38,23 @@ __global__ __launch_bounds__(1024) void order_kernel(unsigned* __restrict__ cost
                                                      int n) {
   __shared__ int hist[256];
   __shared__ int cursor[256];
-  for (int i = threadIdx.x; i < 256; i += 1024) hist[i] = 0;
+  __shared__ int scan[256];
+  const int t = static_cast<int>(threadIdx.x);
+  if (t < 256) hist[t] = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += 1024) atomicAdd(&hist[cost_bucket(cost[i])], 1);
+  for (int i = t; i < n; i += 1024) atomicAdd(&hist[cost_bucket(cost[i])], 1);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int b = 255; b >= 0; --b) {   // descending cost first
-      cursor[b] = run;
-      run += hist[b];
-    }
+  // descending cost first: bucket b's first slot is the count of the buckets
+  // above it (a parallel scan over the reversed histogram, 8 steps)
+  if (t < 256) scan[t] = hist[255 - t];
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int v = (t < 256 && t >= off) ? scan[t - off] : 0;
+    __syncthreads();
+    if (t < 256) scan[t] += v;
+    __syncthreads();
   }
+  if (t < 256) cursor[255 - t] = scan[t] - hist[255 - t];
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += 1024) {
     const unsigned c = cost[i];
