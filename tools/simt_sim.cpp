@@ -17,6 +17,8 @@
 //          waves refilling from it (advanced in cost order)
 //   sort   the 4 waves advance together; before every iteration the 256
 //          paths are sorted by a key and dealt to the waves in that order
+//   pair   (PAIR=R, NV=7 V0=6) R paths per lane, their segments walked back
+//          to back in one traversal loop, then all shaded (round 6)
 //
 //   g++ -O2 -std=c++17 -I include tools/simt_sim.cpp raytracing-clj_amd/csrc/bvh.cpp \
 //       -Lraytracing-clj_amd/lib -lrtclj -Wl,-rpath,$PWD/raytracing-clj_amd/lib -o /tmp/simt_sim
@@ -45,7 +47,8 @@ static double g_disk = 0, g_ball = 0, g_both = 0;   // rejection-loop wave trips
 static double g_abs = 0;   // wave iterations with a metal absorption
 static double C_EXACT_B = 32;
 static double C_BALL = 27, C_DISK = 21;   // one rejection-loop trip (random-unit-vec3, disk)
-static int g_restart_k = 32;   // policy 2: shade once this many lanes finished traversal
+static int g_restart_k = 32;
+static int g_pair = 2;   // policy 3: paths per lane   // policy 2: shade once this many lanes finished traversal
 static int g_charge_rej = 0;   // policies 0/1: add the rejection trips to the cost (RJ=1)
 
 // VALU wave-instructions per block (from the ISA of the default kernel,
@@ -474,6 +477,55 @@ static void run_tile(const Ctx& C, int tx, int ty, int policy, int key_mode, Res
     }
     return;
   }
+  if (policy == 3) {
+    // R paths per lane (lanes [l], [l + NL]...): one loop walks the lane's
+    // segments back to back, then all are shaded
+    const int R2 = g_pair;
+    std::vector<Path> more(NL * (R2 - 1));
+    for (auto& p : more) p.j = next < pool ? next++ : -1;
+    auto P = [&](int l, int r) -> Path& { return r == 0 ? lanes[l] : more[(r - 1) * NL + l]; };
+    std::vector<double> wc(g_nw, 0.0);
+    for (;;) {
+      int w = -1;
+      for (int k = 0; k < g_nw; ++k) {
+        bool any = false;
+        for (int l = 0; l < 64; ++l) for (int r = 0; r < R2; ++r) any |= P(64 * k + l, r).j >= 0;
+        if (any && (w < 0 || wc[k] < wc[w])) w = k;
+      }
+      if (w < 0) break;
+      std::vector<Trav> comb(64);
+      std::vector<const Trav*> act;
+      int nseg_max = 0;
+      for (int l = 0; l < 64; ++l) {
+        int ns = 0;
+        for (int r = 0; r < R2; ++r) {
+          Path& p = P(64 * w + l, r);
+          if (p.j < 0) continue;
+          int px, py;
+          pixel(p.j, px, py);
+          Trav t;
+          const bool end = step(C, p, px, py, t);
+          ++ns;
+          Trav& c = comb[l];
+          c.leaves.insert(c.leaves.end(), t.leaves.begin(), t.leaves.end());
+          c.c1.insert(c.c1.end(), t.c1.begin(), t.c1.end());
+          c.c2.insert(c.c2.end(), t.c2.begin(), t.c2.end());
+          c.big_c |= t.big_c;
+          R.lane_steps += t.leaves.size();
+          if (end) { p = Path{}; p.j = next < pool ? next++ : -1; }
+        }
+        nseg_max = std::max(nseg_max, ns);
+        if (ns) act.push_back(&comb[l]);
+      }
+      double c = wave_cost(act, &R.steps);
+      // outer work (camera/setup/shading) and the big-body leaf once per path slot in use
+      c += (nseg_max - 1) * (C_OUT + (g_big_leaves ? g_big_leaves * C_LEAF : 0.0));
+      wc[w] += c;
+      R.cost += c;
+      R.iters += 1;
+    }
+    return;
+  }
   if (policy == 0) {
     // 4 independent waves, advanced in order of accumulated cost
     std::vector<double> wc(g_nw, 0.0);
@@ -678,8 +730,9 @@ int main(int argc, char** argv) {
     pick.push_back(int(h % uint32_t(gx * (gy - 1))));
   }
   const char* names[] = {"wave (shipped)", "sort by octant", "sort by octant+body", "sort by visits (bound)",
-                         "restart (RK lanes)", "compact (no sort)"};
-  const int pol[] = {0, 1, 1, 1, 2, 1}, km[] = {0, 1, 2, 3, 0, 4};
+                         "restart (RK lanes)", "compact (no sort)", "paths per lane (PAIR)"};
+  const int pol[] = {0, 1, 1, 1, 2, 1, 3}, km[] = {0, 1, 2, 3, 0, 4, 0};
+  if (std::getenv("PAIR")) g_pair = std::atoi(std::getenv("PAIR"));
   if (std::getenv("RJ")) g_charge_rej = std::atoi(std::getenv("RJ"));
   if (std::getenv("RK")) g_restart_k = std::atoi(std::getenv("RK"));
   const int v0 = std::getenv("V0") ? std::atoi(std::getenv("V0")) : 0;
