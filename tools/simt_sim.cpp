@@ -19,6 +19,8 @@
 //          paths are sorted by a key and dealt to the waves in that order
 //   pair   (PAIR=R, NV=7 V0=6) R paths per lane, their segments walked back
 //          to back in one traversal loop, then all shaded (round 6)
+//   DEFER=1 (with any policy): a visit's second leaf pushed and tested as a
+//          leaf-only step next (one leaf pass per step); CNODE overrides C_NODE
 //
 //   g++ -O2 -std=c++17 -I include tools/simt_sim.cpp raytracing-clj_amd/csrc/bvh.cpp \
 //       -Lraytracing-clj_amd/lib -lrtclj -Wl,-rpath,$PWD/raytracing-clj_amd/lib -o /tmp/simt_sim
@@ -333,7 +335,31 @@ static bool step(const Ctx& C, Path& p, int px, int py, Trav& tr) {
 
 // wave cost of one outer iteration over the lanes' segments
 static double g_leaf_passes = 0, g_exact_passes = 0;
-static double wave_cost(const std::vector<const Trav*>& lanes, double* node_steps) {
+static int g_defer = 0;
+static double wave_cost0(const std::vector<const Trav*>& lanes, double* node_steps);
+static double wave_cost(const std::vector<const Trav*>& lanes0, double* node_steps) {
+  if (!g_defer) return wave_cost0(lanes0, node_steps);
+  // the second leaf of a two-leaf visit is pushed and popped at the next step
+  // as a leaf-only step (its own single pass, shared with other lanes' first leaves)
+  std::vector<Trav> tt(lanes0.size());
+  std::vector<const Trav*> lanes;
+  for (size_t k = 0; k < lanes0.size(); ++k) {
+    const Trav& a = *lanes0[k];
+    Trav& t = tt[k];
+    t.disk_tries = a.disk_tries; t.ball_tries = a.ball_tries; t.absorbed = a.absorbed; t.big_c = a.big_c;
+    for (size_t i = 0; i < a.leaves.size(); ++i) {
+      if (a.leaves[i] == 2) {
+        t.leaves.push_back(1); t.c1.push_back(a.c1[i]); t.c2.push_back(0);
+        t.leaves.push_back(1); t.c1.push_back(a.c2[i]); t.c2.push_back(0);
+      } else {
+        t.leaves.push_back(a.leaves[i]); t.c1.push_back(a.c1[i]); t.c2.push_back(a.c2[i]);
+      }
+    }
+    lanes.push_back(&t);
+  }
+  return wave_cost0(lanes, node_steps);
+}
+static double wave_cost0(const std::vector<const Trav*>& lanes, double* node_steps) {
   if (lanes.empty()) return 0.0;
   size_t L = 0;
   int mb = 0, ob = 0, md = 0, mball = 0, mboth = 0, anyabs = 0;
@@ -732,6 +758,8 @@ int main(int argc, char** argv) {
   const char* names[] = {"wave (shipped)", "sort by octant", "sort by octant+body", "sort by visits (bound)",
                          "restart (RK lanes)", "compact (no sort)", "paths per lane (PAIR)"};
   const int pol[] = {0, 1, 1, 1, 2, 1, 3}, km[] = {0, 1, 2, 3, 0, 4, 0};
+  if (std::getenv("DEFER")) g_defer = std::atoi(std::getenv("DEFER"));
+  if (std::getenv("CNODE")) C_NODE = std::atof(std::getenv("CNODE"));
   if (std::getenv("PAIR")) g_pair = std::atoi(std::getenv("PAIR"));
   if (std::getenv("RJ")) g_charge_rej = std::atoi(std::getenv("RJ"));
   if (std::getenv("RK")) g_restart_k = std::atoi(std::getenv("RK"));
