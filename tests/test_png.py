@@ -87,3 +87,40 @@ def test_io_errors(R, tmp_path):
     with pytest.raises(RTError) as e:
         R.write_png(tmp_path / "no" / "dir.png", np.zeros((2, 2, 3), np.uint8))
     assert e.value.code == -6
+
+
+def test_ppm_to_png_parses_a_large_frame_in_spans(R, tmp_path):
+    """A frame whose text spans several parse spans (~1 MB each): the PNG
+    equals rt_write_png's of the same pixels, and text after the last pixel
+    is ignored (as a sequential parse ignores it)."""
+    rng = np.random.default_rng(7)
+    pix = rng.integers(0, 256, (450, 800, 3), dtype=np.uint8)
+    R.write_ppm(tmp_path / "s.ppm", pix)
+    assert (tmp_path / "s.ppm").stat().st_size > 3 << 20
+    R.ppm_to_png(tmp_path / "s.ppm", tmp_path / "a.png")
+    R.write_png(tmp_path / "b.png", pix)
+    assert (tmp_path / "a.png").read_bytes() == (tmp_path / "b.png").read_bytes()
+    with open(tmp_path / "s.ppm", "a") as f:
+        f.write("trailing x 999 words\n")
+    R.ppm_to_png(tmp_path / "s.ppm", tmp_path / "c.png")
+    assert (tmp_path / "c.png").read_bytes() == (tmp_path / "b.png").read_bytes()
+
+
+@pytest.mark.parametrize("bad_pixel,token", [(3, "x"), (200_000, "256"), (359_999, "1234567890")])
+def test_ppm_to_png_reports_the_first_bad_pixel_in_any_span(R, tmp_path, bad_pixel, token):
+    """A bad token early, in a middle span and at the last pixel: the error
+    names the pixel a sequential parse stops at."""
+    from rtclj import RTError
+    rng = np.random.default_rng(bad_pixel)
+    pix = rng.integers(0, 256, (450, 800, 3), dtype=np.uint8)
+    lines = ["P3", "800 450", "255"] + [" ".join(map(str, p)) for p in pix.reshape(-1, 3)]
+    lines[3 + bad_pixel] = f"1 {token} 2"
+    later = min(bad_pixel + 70_000, 359_999)
+    if later > bad_pixel:
+        lines[3 + later] = "0 -1 0"                     # a later bad token, in a later span: not the one named
+    (tmp_path / "bad.ppm").write_text("\n".join(lines) + "\n0 0 q\n")
+    with pytest.raises(RTError) as e:
+        R.ppm_to_png(tmp_path / "bad.ppm", tmp_path / "bad.png")
+    assert e.value.code == -1
+    assert f"bad pixel value at {bad_pixel}" in str(e.value)
+    assert not (tmp_path / "bad.png").exists()
