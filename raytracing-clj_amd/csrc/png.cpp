@@ -117,7 +117,7 @@ std::vector<uint8_t> filter_rows(const uint8_t* rgb, int w, int h) {
   const size_t stride = static_cast<size_t>(w) * 3;
   std::vector<uint8_t> out((stride + 1) * static_cast<size_t>(h));
   std::vector<uint8_t> zero(stride, 0);
-  constexpr int kRowsPerTask = 32;
+  constexpr int kRowsPerTask = 16;
   parallel_for((h + kRowsPerTask - 1) / kRowsPerTask, [&](int task) {
     for (int y = task * kRowsPerTask; y < std::min(h, (task + 1) * kRowsPerTask); ++y)
       filter_row(rgb + stride * y, y > 0 ? rgb + stride * (y - 1) : zero.data(), stride,
@@ -143,7 +143,7 @@ struct ZStream {
 constexpr uint8_t kZlibHeader[2] = {0x78, 0x9c};
 
 bool deflate_chunked(const std::vector<uint8_t>& raw, ZStream* z) {
-  constexpr size_t kChunk = 256 * 1024;
+  constexpr size_t kChunk = 64 * 1024;   // (deflate's window is 32 KB: chunks this size lose little)
   const size_t n = raw.size();
   const int nchunk = static_cast<int>(std::max<size_t>(1, (n + kChunk - 1) / kChunk));
   z->part.assign(nchunk, {});
@@ -152,9 +152,11 @@ bool deflate_chunked(const std::vector<uint8_t>& raw, ZStream* z) {
   parallel_for(nchunk, [&](int c) {
     const size_t b = static_cast<size_t>(c) * kChunk, len = std::min(kChunk, n - b);
     z_stream zs{};
-    // level 1: a C1 frame in ~1/2.5 of level 6's time for a 13 % larger file
-    // (the bytes are a lossless encoding either way; the pixels are the PPM's)
-    if (deflateInit2(&zs, 1, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+    // Z_RLE (runs of the filtered bytes, then Huffman codes): C1's rendered
+    // frame in 28 ms of one core against 50 for level 1's LZ77 and 203 for
+    // level 6, and 996 KB against 1,065 / 991 (tools/png_stages.cpp; the
+    // bytes are a lossless encoding either way, the pixels are the PPM's)
+    if (deflateInit2(&zs, 1, Z_DEFLATED, -15, 8, Z_RLE) != Z_OK) {
       ok = false;
       return;
     }
@@ -224,7 +226,7 @@ extern "C" int rt_write_png(const char* path, const uint8_t* rgb, int width, int
 // colour value in [0, 255], then width*height pixels of three values (the
 // reference reads one pixel per line; any whitespace is accepted here).
 // Values are written as they are (ppm2png packs r<<16|g<<8|b unscaled).
-// The pixel values (2.4 M numbers in a C1 frame) are parsed in parallel:
+// The pixel values (2.4 M numbers, 9 MB of text in a C1 frame) are parsed in parallel:
 // the text is cut at whitespace into one span per thread, each span's values
 // parsed into its own buffer, then placed by the spans' counts; an error is
 // the first one in text order, reported at its pixel as a sequential parse
@@ -265,12 +267,16 @@ extern "C" int rt_ppm_to_png(const char* src, const char* dst) {
   FILE* f = std::fopen(src, "rb");
   if (!f) return rtclj::set_error(RT_E_IO, std::string("rt_ppm_to_png: cannot open ") + src);
   std::string text;
-  if (std::fseek(f, 0, SEEK_END) == 0) {   // (one read of the whole file where its size is known)
-    const long sz = std::ftell(f);
-    if (sz > 0) text.reserve(static_cast<size_t>(sz));
-    std::fseek(f, 0, SEEK_SET);
+  long sz = -1;
+  if (std::fseek(f, 0, SEEK_END) == 0) {   // (one read straight into the text where the size is known)
+    sz = std::ftell(f);
+    if (std::fseek(f, 0, SEEK_SET) != 0) sz = -1;
   }
-  char buf[1 << 16];
+  if (sz > 0) {
+    text.resize(static_cast<size_t>(sz));
+    text.resize(std::fread(&text[0], 1, text.size(), f));
+  }
+  char buf[1 << 16];   // (the rest, or a stream of unknown size)
   for (size_t n; (n = std::fread(buf, 1, sizeof buf, f)) > 0;) text.append(buf, n);
   std::fclose(f);
   size_t pos = 0;
@@ -286,9 +292,10 @@ extern "C" int rt_ppm_to_png(const char* src, const char* dst) {
   if (!parse_number(t, tn, &pos, &maxv) || maxv > 255)
     return rtclj::set_error(RT_E_ARG, std::string("rt_ppm_to_png: ") + src + ": bad colour size");
   const size_t need = static_cast<size_t>(w) * h * 3;
-  // spans of ~1 MB (at least one), cut at whitespace so no token is split
+  // spans of ~256 KB (at least one, at most 256), cut at whitespace so no
+  // token is split
   const size_t body = tn - pos;
-  const int nspan = static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, body >> 20)));
+  const int nspan = static_cast<int>(std::max<size_t>(1, std::min<size_t>(256, body >> 18)));
   std::vector<size_t> cut(nspan + 1);
   cut[0] = pos;
   cut[nspan] = tn;

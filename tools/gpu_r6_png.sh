@@ -15,6 +15,7 @@ for i in 1 2 3; do
 done > "$OUT/stages.txt"
 cmp /tmp/o.png /tmp/n.png && cmp /tmp/o.png.direct.png /tmp/n.png.direct.png && echo "png bytes identical" >> "$OUT/stages.txt"
 ls -l /tmp/c1.ppm /tmp/n.png >> "$OUT/stages.txt"
+cp /tmp/c1.ppm "$OUT/c1.ppm"
 for i in 1 2 3; do
   timeout -k 10 60 raytracing-clj_amd/lib/rt_main 100 50 --scene cover --width 1200 --seed 1 --gpus 1 --json \
     --out /tmp/c1b.ppm > "$OUT/rt_main_$i.json" || exit 1
