@@ -497,24 +497,38 @@ def first_process(wl, spp, depth, seed, n_dev):
     fresh child process on this workload (the cover scene), --json: the HIP
     runtime's start-up (first rt_device_count), rt_render's parts on a cold
     library (scene upload + BVHs, device context, first launch = code-object
-    load, kernel in plain tile order + D2H), quantise and the PPM write."""
+    load, kernel in plain tile order + D2H), quantise and the PPM write.
+    `next_process`: a second fresh process right after it.  (On a fresh box
+    the first such child has paid ~140 ms more in its first allocation +
+    launch + sync -- prepare_ms.queue -- than the ones after it,
+    profiles/r06/final/bench_reps.jsonl: the runtime's, not the library's.)"""
     import subprocess
     import tempfile
     exe = ROOT / "raytracing-clj_amd" / "lib" / "rt_main"
     if wl["scene"] != "cover11" or not exe.exists():
         return None
-    with tempfile.TemporaryDirectory() as td:
-        t0 = time.perf_counter()
-        extra = ["--rejection-samplers"] if SAMPLER_FLAGS & RT_FLAG_REJECTION_SAMPLERS else []
-        r = subprocess.run([str(exe), str(spp), str(depth), "--scene", "cover", "--width", str(wl["width"]),
-                            "--seed", str(seed), "--gpus", str(n_dev), "--out", str(Path(td) / "scene.ppm"), "--json"]
-                           + extra, capture_output=True, text=True, timeout=300)
-        wall = (time.perf_counter() - t0) * 1e3
-    if r.returncode != 0:
-        return {"error": (r.stdout + r.stderr)[-400:]}
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    d["child_wall_ms"] = wall
+    extra = ["--rejection-samplers"] if SAMPLER_FLAGS & RT_FLAG_REJECTION_SAMPLERS else []
+
+    def one():
+        with tempfile.TemporaryDirectory() as td:
+            t0 = time.perf_counter()
+            r = subprocess.run([str(exe), str(spp), str(depth), "--scene", "cover", "--width", str(wl["width"]),
+                                "--seed", str(seed), "--gpus", str(n_dev), "--out", str(Path(td) / "scene.ppm"),
+                                "--json"] + extra, capture_output=True, text=True, timeout=300)
+            wall = (time.perf_counter() - t0) * 1e3
+        if r.returncode != 0:
+            return {"error": (r.stdout + r.stderr)[-400:]}
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d["child_wall_ms"] = wall
+        return d
+    d = one()
+    if "error" in d:
+        return d
     d["command"] = f"rt_main {spp} {depth} --scene cover --width {wl['width']} --seed {seed} --gpus {n_dev} --json"
+    nxt = one()
+    d["next_process"] = nxt if "error" in nxt else {
+        k: nxt[k] for k in ("process_ms", "device_count_ms", "prepare_ms", "prepare_wait_ms", "render_ms",
+                            "write_ms", "png_ms", "child_wall_ms")}
     return d
 
 
